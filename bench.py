@@ -1,0 +1,227 @@
+#!/usr/bin/env python3
+"""bench.py -- headline benchmark: batched forward NTT/s (N = 2^16, L = 8, batch = 1024) on MI355X.
+
+Workload (BASELINE.json configs[2], the N = 2^16 configuration the metric is quoted on):
+  one step = one batched forward negacyclic NTT (phantom convention, mfhe_ntt_fwd) over a
+  [1024][8][65536] u64 residue batch (4 GiB) resident in HBM.  Secondary line items:
+  inverse NTT and encode+CRT ops/s (RNS decompose + wide CRT compose -> f64) on the same shape.
+
+Multi-GPU: one process per GPU (torchrun), residue-batch sharding -- every rank transforms its own
+batch (weak scaling), no data-path collective; barrier + max-over-ranks timing.
+
+Run: python bench.py [--gpus N --steps K --warmup W]
+"""
+from __future__ import annotations
+
+import argparse
+import ctypes
+import json
+import os
+import sys
+import time
+from pathlib import Path
+
+ROOT = Path(__file__).resolve().parent
+sys.path.insert(0, str(ROOT / "matrix-fhe-gpu_amd"))
+
+HBM_PEAK_GBS = 8000.0   # MI355X HBM3E spec (/opt/skills/guides/MI355X_MICROARCH.md)
+
+
+def parse():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=20)
+    ap.add_argument("--warmup", type=int, default=3)
+    ap.add_argument("--log-n", type=int, default=16)
+    ap.add_argument("--limbs", type=int, default=8)
+    ap.add_argument("--batch", type=int, default=1024)
+    ap.add_argument("--arith", type=int, default=0, help="0 auto, 1 f64, 2 u64")
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--cpu-seconds", type=float, default=10.0)
+    ap.add_argument("--only", default="all", help="all | ntt | crt (profiling)")
+    return ap.parse_args()
+
+
+def gen_moduli(bits, m, count):
+    """Largest `count` primes q < 2^bits with q = 1 mod m (deterministic; same as the oracle's)."""
+    out = []
+    c = ((2 ** bits - 2) // m) * m + 1
+    while len(out) < count:
+        if is_prime(c):
+            out.append(c)
+        c -= m
+    return out
+
+
+def is_prime(n):
+    if n < 2:
+        return False
+    for p in (2, 3, 5, 7, 11, 13, 17, 19, 23, 29, 31, 37):
+        if n % p == 0:
+            return n == p
+    d, s = n - 1, 0
+    while d % 2 == 0:
+        d //= 2
+        s += 1
+    for a in (2, 3, 5, 7, 11, 13, 17, 19, 23, 29, 31, 37):
+        x = pow(a, d, n)
+        if x in (1, n - 1):
+            continue
+        for _ in range(s - 1):
+            x = x * x % n
+            if x == n - 1:
+                break
+        else:
+            return False
+    return True
+
+
+def cpu_baseline(log_n, moduli, seconds):
+    """Reference CPU path restated (oracle, Harvey/Shoup phantom NTT, OpenMP over polys)."""
+    import numpy as np
+    sys.path.insert(0, str(ROOT / "tests"))
+    import oracle
+    N = 1 << log_n
+    L = len(moduli)
+    threads = int(os.environ.get("OMP_NUM_THREADS", os.cpu_count() or 1))
+    rng = np.random.default_rng(0)
+    q = np.array(moduli, np.uint64)[None, :, None]
+    data = (rng.integers(0, 2 ** 63, (1, L, N), dtype=np.uint64) % q).ravel()
+    probe = np.tile(data, 8)
+    oracle.phantom_fwd(probe, L, log_n, moduli)          # warm (tables, threads)
+    t0 = time.perf_counter()
+    oracle.phantom_fwd(probe, L, log_n, moduli)
+    one = max((time.perf_counter() - t0) / 8, 1e-5)
+    batch = max(1, int(seconds / one))
+    data = np.tile(data, batch)
+    t0 = time.perf_counter()
+    oracle.phantom_fwd(data, L, log_n, moduli)
+    dt = time.perf_counter() - t0
+    return {"value": batch * L / dt, "unit": "NTT/s", "cores": threads, "kind": "port",
+            "sample": f"{batch}x{L} forward NTTs N=2^{log_n} (oracle phantom Harvey NTT, OpenMP {threads} threads, "
+                      f"{dt:.1f} s)"}
+
+
+def main():
+    args = parse()
+    import torch
+    import torch.distributed as dist
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world > 1:
+        torch.cuda.set_device(local)
+        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+    dev = torch.device("cuda", local)
+    torch.cuda.set_device(dev)
+
+    import mfhe
+
+    log_n, L, batch = args.log_n, args.limbs, args.batch
+    N = 1 << log_n
+    moduli = gen_moduli(50, 1 << (log_n + 2), L)
+    ctx = mfhe.Context(moduli, log_n, mfhe.CONV_PHANTOM)
+    if args.arith:
+        ctx.set_arith(args.arith)
+    stream = torch.cuda.current_stream()
+
+    # synthetic residues uniform in [0, q_l), generated on device
+    g = torch.Generator(device=dev).manual_seed(0x4D46484500000000 % (2 ** 63) + 3 + rank)
+    data = torch.empty(batch * L * N, dtype=torch.int64, device=dev)
+    qt = torch.tensor(moduli, dtype=torch.int64, device=dev).repeat_interleave(N).repeat(batch)
+    data.random_(0, 2 ** 62, generator=g)
+    data.remainder_(qt)
+    del qt
+
+    def barrier():
+        if world > 1:
+            dist.barrier()
+        torch.cuda.synchronize()
+
+    def timed(fn, steps, warmup):
+        for _ in range(warmup):
+            fn()
+        barrier()
+        ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        t0 = time.perf_counter()
+        ev0.record(stream)
+        for _ in range(steps):
+            fn()
+        ev1.record(stream)
+        barrier()
+        wall = time.perf_counter() - t0
+        ev_ms = ev0.elapsed_time(ev1)
+        t = torch.tensor([wall], dtype=torch.float64, device=dev)
+        if world > 1:
+            dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        return t.item(), ev_ms / steps
+
+    res = {}
+    if args.only in ("all", "ntt"):
+        wall, ev_ms = timed(lambda: ctx.ntt_fwd(data, batch=batch, stream=stream), args.steps, args.warmup)
+        res["fwd_wall"], res["fwd_ev_ms"] = wall, ev_ms
+        wall_i, ev_i = timed(lambda: ctx.ntt_inv(data, batch=batch, stream=stream), max(1, args.steps // 2), 1)
+        res["inv_ev_ms"] = ev_i
+    if args.only in ("all", "crt"):
+        # encode+CRT op = one real poly of N coefficients: decompose (f64 -> L residues) + compose (-> f64/delta)
+        cb = max(1, batch // 4)
+        z = torch.rand(cb * N, dtype=torch.float64, device=dev, generator=g) * 2 - 1
+        r = data[: cb * L * N]
+        zo = torch.empty_like(z)
+
+        def enc_crt():
+            ctx.rns_decompose(z, r, cb, N, stream=stream)
+            ctx.crt_compose_f64(r, zo, cb, N, stream=stream)
+
+        wall_c, ev_c = timed(enc_crt, max(1, args.steps // 2), 1)
+        res["crt_ev_ms"], res["crt_batch"] = ev_c, cb
+
+    if rank == 0:
+        ntts = batch * L * world
+        out = {
+            "metric": "forward-NTT/s (N=2^16, L RNS limbs)",
+            "unit": "NTT/s",
+            "n_gpus": world,
+            "steps": args.steps,
+            "warmup": args.warmup,
+            "higher_is_better": True,
+            "scaling": "weak",
+            "vs_baseline": None,
+            "dtype": "u64",
+            "data": "synthetic uniform residues in [0, q_l), device-resident",
+            "config": {"workload": f"batched forward negacyclic NTT (phantom convention), N=2^{log_n}, "
+                                   f"L={L} x 50-bit primes, batch={batch} per GPU",
+                       "N": N, "limbs": L, "batch_per_gpu": batch,
+                       "arith": "f64" if ctx.info().arith == mfhe.ARITH_F64 else "u64",
+                       "parallelism": f"residue-batch shard x{world} (no collective)"},
+        }
+        if "fwd_wall" in res:
+            step_s = res["fwd_wall"] / args.steps
+            out["value"] = ntts / step_s
+            out["ms_per_step"] = step_s * 1e3
+            alg_bytes = 16.0 * N * batch * L       # 8N read + 8N write per NTT
+            ach = alg_bytes / (res["fwd_ev_ms"] * 1e-3) / 1e9
+            out["roofline"] = {"bound": "hbm", "kernel": "mfhe_ntt_fwd (2 launches: column pass + block pass)",
+                               "achieved": round(ach, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                               "frac": round(ach / HBM_PEAK_GBS, 4), "traffic": None,
+                               "algorithmic_bytes_per_launch": alg_bytes,
+                               "hbm_read_frac": round(ach / 2 / HBM_PEAK_GBS, 4),
+                               "event_ms_per_transform": round(res["fwd_ev_ms"], 4)}
+            out["inverse_NTT_per_s"] = batch * L / (res["inv_ev_ms"] * 1e-3) * world
+        if "crt_ev_ms" in res:
+            cb = res["crt_batch"]
+            out["encode_crt_ops_per_s"] = cb / (res["crt_ev_ms"] * 1e-3) * world
+            out["encode_crt_GBps"] = 16.0 * (L + 1) * N * cb / (res["crt_ev_ms"] * 1e-3) / 1e9
+        if world == 1 and not args.no_cpu_baseline and args.only == "all":
+            try:
+                out["cpu_baseline"] = cpu_baseline(log_n, moduli, args.cpu_seconds)
+            except Exception as e:  # reported, never fatal
+                out["cpu_baseline"] = {"error": str(e)}
+        print(json.dumps(out), flush=True)
+    if world > 1:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

@@ -1,0 +1,288 @@
+// crt.hip -- RNS decompose and wide CRT compose / centre-lift / f64 for gfx950.
+//
+// Reference semantics:
+//   decompose : quantize_coeff_to_rns_kernel (batched_encoder.cu:125-152):
+//               x = llround(z*delta) as int64; r = x % q (C truncation) + q if negative
+//   compose   : crt_compose_centerlift_big_kernel (encoder.cu:191-230):
+//               acc = sum_k M_k * ((x_k * inv_k) mod q_k) mod Q; centre-lift against Q/2
+//   to_f64    : he_big_to_f64 + compose_big_pair_to_complex_by_delta (HE.cu:917-924, 1007-1027)
+//
+// Design: one thread per coefficient, all W words of the accumulator in
+// registers (W is a template parameter, 1..32), the mod-Q reduction done once
+// with an FP64 quotient estimate floor(sum_k t_k/q_k) and a single +-Q
+// correction instead of the reference's per-limb compare/subtract.  Inputs are
+// read limb-major so every load instruction is coalesced; the per-limb tables
+// (M_k, inv_k, 1/q_k) are wave-uniform and come through the scalar cache.
+#include <hip/hip_runtime.h>
+
+#include "mfhe_ctx.hpp"
+
+namespace mfhe {
+
+using u128 = unsigned __int128;
+
+// ---------------- RNS decompose ----------------
+__global__ __launch_bounds__(256) void rns_decompose_kernel(const double* __restrict__ in, uint64_t in_stride,
+                                                            uint64_t total, uint64_t ncoeff, int L,
+                                                            const uint64_t* __restrict__ qmu, double delta,
+                                                            uint64_t* __restrict__ out) {
+    const uint64_t i = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x;
+    if (i >= total) return;
+    const uint64_t p = i / ncoeff, c = i - p * ncoeff;
+    const double z = in[i * in_stride] * delta;
+    const long long x = llround(z);
+    const bool neg = x < 0;
+    const uint64_t ax = neg ? (uint64_t)0 - (uint64_t)x : (uint64_t)x;
+    uint64_t* o = out + p * (uint64_t)L * ncoeff + c;
+    for (int l = 0; l < L; ++l) {
+        const uint64_t q = qmu[2 * l], mu = qmu[2 * l + 1];
+        uint64_t r = ax - __umul64hi(ax, mu) * q;   // Barrett: [0, 2q)
+        r = r >= q ? r - q : r;
+        r = (neg && r) ? q - r : r;
+        o[(uint64_t)l * ncoeff] = r;
+    }
+}
+
+// ---------------- wide CRT compose ----------------
+template <int W>
+__device__ __forceinline__ void compose_one(const uint64_t* __restrict__ in, uint64_t ncoeff, int L,
+                                            const uint64_t* __restrict__ qmu, const uint64_t* __restrict__ inv,
+                                            const double* __restrict__ qinv, const uint64_t* __restrict__ M,
+                                            const uint64_t* __restrict__ Q, const uint64_t* __restrict__ Qh,
+                                            uint64_t (&mag)[W], bool& neg) {
+    uint64_t acc[W + 1];
+#pragma unroll
+    for (int i = 0; i <= W; ++i) acc[i] = 0;
+    double est = 0.0;
+    for (int k = 0; k < L; ++k) {
+        const uint64_t q = qmu[2 * k];
+        const uint64_t x = in[(uint64_t)k * ncoeff];
+        uint64_t t = x * inv[2 * k] - __umul64hi(x, inv[2 * k + 1]) * q;   // Shoup: [0, 2q)
+        t = t >= q ? t - q : t;
+        est += (double)t * qinv[k];
+        const uint64_t* Mk = M + (size_t)k * W;
+        uint64_t carry = 0;
+#pragma unroll
+        for (int i = 0; i < W; ++i) {
+            const u128 pr = (u128)t * Mk[i] + acc[i] + carry;
+            acc[i] = (uint64_t)pr;
+            carry = (uint64_t)(pr >> 64);
+        }
+        acc[W] += carry;
+    }
+    // subtract e*Q, e = floor(sum t_k / q_k) (exact or off by one)
+    const uint64_t e = (uint64_t)__builtin_floor(est);
+    {
+        uint64_t carry = 0, borrow = 0;
+#pragma unroll
+        for (int i = 0; i <= W; ++i) {
+            const u128 pr = (u128)e * (i < W ? Q[i] : 0) + carry;
+            const uint64_t s = (uint64_t)pr;
+            carry = (uint64_t)(pr >> 64);
+            const uint64_t a = acc[i];
+            const uint64_t d = a - s - borrow;
+            borrow = (a < s) || (a - s < borrow);
+            acc[i] = d;
+        }
+    }
+    // result r in (-Q, 2Q): fix to [0, Q)
+    if ((int64_t)acc[W] < 0) {
+        uint64_t c = 0;
+#pragma unroll
+        for (int i = 0; i <= W; ++i) {
+            const u128 s = (u128)acc[i] + (i < W ? Q[i] : 0) + c;
+            acc[i] = (uint64_t)s;
+            c = (uint64_t)(s >> 64);
+        }
+    } else {
+        bool ge = acc[W] != 0;
+        if (!ge) {
+            ge = true;  // equal counts as >=
+#pragma unroll
+            for (int i = W - 1; i >= 0; --i) {
+                if (acc[i] != Q[i]) { ge = acc[i] > Q[i]; break; }
+            }
+        }
+        if (ge) {
+            uint64_t b = 0;
+#pragma unroll
+            for (int i = 0; i < W; ++i) {
+                const uint64_t a = acc[i], s = Q[i];
+                acc[i] = a - s - b;
+                b = (a < s) || (a - s < b);
+            }
+        }
+    }
+    // centre lift against Q_half = floor(Q/2)
+    bool gt = false;
+#pragma unroll
+    for (int i = W - 1; i >= 0; --i) {
+        if (acc[i] != Qh[i]) { gt = acc[i] > Qh[i]; break; }
+    }
+    neg = gt;
+    if (gt) {
+        uint64_t b = 0;
+#pragma unroll
+        for (int i = 0; i < W; ++i) {
+            const uint64_t a = Q[i], s = acc[i];
+            mag[i] = a - s - b;
+            b = (a < s) || (a - s < b);
+        }
+    } else {
+#pragma unroll
+        for (int i = 0; i < W; ++i) mag[i] = acc[i];
+    }
+}
+
+template <int W>
+__device__ __forceinline__ double big_to_f64(const uint64_t (&mag)[W], bool neg, double delta) {
+    const double two64 = 18446744073709551616.0;
+    double v = 0.0;
+#pragma unroll
+    for (int i = W - 1; i >= 0; --i) v = v * two64 + (double)mag[i];
+    if (neg) v = -v;
+    return v / delta;
+}
+
+struct CrtArgs {
+    const uint64_t* in;
+    uint64_t ncoeff, total;
+    int L;
+    const uint64_t *qmu, *inv;
+    const double* qinv;
+    const uint64_t *M, *Q, *Qh;
+};
+
+template <int W>
+__global__ __launch_bounds__(256) void crt_compose_kernel(CrtArgs a, uint64_t* __restrict__ out_mag,
+                                                          uint8_t* __restrict__ out_neg) {
+    const uint64_t i = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x;
+    if (i >= a.total) return;
+    const uint64_t p = i / a.ncoeff, c = i - p * a.ncoeff;
+    uint64_t mag[W];
+    bool neg;
+    compose_one<W>(a.in + p * (uint64_t)a.L * a.ncoeff + c, a.ncoeff, a.L, a.qmu, a.inv, a.qinv, a.M, a.Q, a.Qh, mag, neg);
+    uint64_t* o = out_mag + i * W;
+#pragma unroll
+    for (int w = 0; w < W; ++w) o[w] = mag[w];
+    out_neg[i] = neg ? 1 : 0;
+}
+
+template <int W>
+__global__ __launch_bounds__(256) void crt_compose_f64_kernel(CrtArgs a, double delta, double* __restrict__ out,
+                                                              uint64_t out_stride) {
+    const uint64_t i = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x;
+    if (i >= a.total) return;
+    const uint64_t p = i / a.ncoeff, c = i - p * a.ncoeff;
+    uint64_t mag[W];
+    bool neg;
+    compose_one<W>(a.in + p * (uint64_t)a.L * a.ncoeff + c, a.ncoeff, a.L, a.qmu, a.inv, a.qinv, a.M, a.Q, a.Qh, mag, neg);
+    out[i * out_stride] = big_to_f64<W>(mag, neg, delta);
+}
+
+template <int W>
+__global__ __launch_bounds__(256) void crt_to_f64_kernel(const uint64_t* __restrict__ mag_in,
+                                                         const uint8_t* __restrict__ neg_in, uint64_t total,
+                                                         double delta, double* __restrict__ out, uint64_t out_stride) {
+    const uint64_t i = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x;
+    if (i >= total) return;
+    uint64_t mag[W];
+#pragma unroll
+    for (int w = 0; w < W; ++w) mag[w] = mag_in[i * W + w];
+    out[i * out_stride] = big_to_f64<W>(mag, neg_in[i] != 0, delta);
+}
+
+#define MFHE_W_CASES(X) \
+    X(1) X(2) X(3) X(4) X(5) X(6) X(7) X(8) X(9) X(10) X(11) X(12) X(13) X(14) X(15) X(16) \
+    X(17) X(18) X(19) X(20) X(21) X(22) X(23) X(24) X(25) X(26) X(27) X(28) X(29) X(30) X(31) X(32)
+
+static CrtArgs crt_args(const mfhe_ctx* c, const uint64_t* in, uint64_t npoly, uint64_t ncoeff) {
+    CrtArgs a;
+    a.in = in;
+    a.ncoeff = ncoeff;
+    a.total = npoly * ncoeff;
+    a.L = c->L;
+    a.qmu = c->d_rns_mu;
+    a.inv = c->d_crt_inv;
+    a.qinv = c->d_crt_qinv;
+    a.M = c->d_crt_M;
+    a.Q = c->d_crt_Q;
+    a.Qh = c->d_crt_Qhalf;
+    return a;
+}
+
+static inline dim3 grid1d(uint64_t total, uint32_t th) { return dim3((uint32_t)((total + th - 1) / th)); }
+
+}  // namespace mfhe
+
+using namespace mfhe;
+
+extern "C" int mfhe_rns_decompose(mfhe_ctx* c, const double* in, size_t in_stride, size_t npoly, size_t ncoeff,
+                                  uint64_t* out, mfhe_stream_t s) {
+    if (!c) return set_error(MFHE_EINVAL, "null ctx");
+    const uint64_t total = (uint64_t)npoly * ncoeff;
+    if (total == 0) return MFHE_OK;
+    if (!in || !out || in_stride == 0) return set_error(MFHE_EINVAL, "mfhe_rns_decompose: bad pointer/stride");
+    hipLaunchKernelGGL(rns_decompose_kernel, grid1d(total, 256), dim3(256), 0, (hipStream_t)s, in, (uint64_t)in_stride,
+                       total, (uint64_t)ncoeff, c->L, c->d_rns_mu, c->delta, out);
+    MFHE_CHECK_LAUNCH("rns_decompose_kernel");
+    return MFHE_OK;
+}
+
+extern "C" int mfhe_crt_compose(mfhe_ctx* c, const uint64_t* in, size_t npoly, size_t ncoeff, uint64_t* mag,
+                                uint8_t* neg, mfhe_stream_t s) {
+    if (!c) return set_error(MFHE_EINVAL, "null ctx");
+    const uint64_t total = (uint64_t)npoly * ncoeff;
+    if (total == 0) return MFHE_OK;
+    if (!in || !mag || !neg) return set_error(MFHE_EINVAL, "mfhe_crt_compose: null pointer");
+    const CrtArgs a = crt_args(c, in, npoly, ncoeff);
+    switch (c->W) {
+#define X(w) \
+    case w: hipLaunchKernelGGL(crt_compose_kernel<w>, grid1d(total, 256), dim3(256), 0, (hipStream_t)s, a, mag, neg); break;
+        MFHE_W_CASES(X)
+#undef X
+        default: return set_error(MFHE_EUNSUPPORTED, "crt words > 32");
+    }
+    MFHE_CHECK_LAUNCH("crt_compose_kernel");
+    return MFHE_OK;
+}
+
+extern "C" int mfhe_crt_compose_f64(mfhe_ctx* c, const uint64_t* in, size_t npoly, size_t ncoeff, double* out,
+                                    size_t out_stride, mfhe_stream_t s) {
+    if (!c) return set_error(MFHE_EINVAL, "null ctx");
+    const uint64_t total = (uint64_t)npoly * ncoeff;
+    if (total == 0) return MFHE_OK;
+    if (!in || !out || out_stride == 0) return set_error(MFHE_EINVAL, "mfhe_crt_compose_f64: bad pointer/stride");
+    const CrtArgs a = crt_args(c, in, npoly, ncoeff);
+    switch (c->W) {
+#define X(w)                                                                                                       \
+    case w:                                                                                                        \
+        hipLaunchKernelGGL(crt_compose_f64_kernel<w>, grid1d(total, 256), dim3(256), 0, (hipStream_t)s, a, c->delta, \
+                           out, (uint64_t)out_stride);                                                            \
+        break;
+        MFHE_W_CASES(X)
+#undef X
+        default: return set_error(MFHE_EUNSUPPORTED, "crt words > 32");
+    }
+    MFHE_CHECK_LAUNCH("crt_compose_f64_kernel");
+    return MFHE_OK;
+}
+
+extern "C" int mfhe_crt_to_f64(mfhe_ctx* c, const uint64_t* mag, const uint8_t* neg, size_t count, double* out,
+                               size_t out_stride, mfhe_stream_t s) {
+    if (!c) return set_error(MFHE_EINVAL, "null ctx");
+    if (count == 0) return MFHE_OK;
+    if (!mag || !neg || !out || out_stride == 0) return set_error(MFHE_EINVAL, "mfhe_crt_to_f64: bad pointer/stride");
+    switch (c->W) {
+#define X(w)                                                                                                     \
+    case w:                                                                                                      \
+        hipLaunchKernelGGL(crt_to_f64_kernel<w>, grid1d(count, 256), dim3(256), 0, (hipStream_t)s, mag, neg,     \
+                           (uint64_t)count, c->delta, out, (uint64_t)out_stride);                                \
+        break;
+        MFHE_W_CASES(X)
+#undef X
+        default: return set_error(MFHE_EUNSUPPORTED, "crt words > 32");
+    }
+    MFHE_CHECK_LAUNCH("crt_to_f64_kernel");
+    return MFHE_OK;
+}

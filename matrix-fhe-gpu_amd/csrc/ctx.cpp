@@ -1,0 +1,324 @@
+// ctx.cpp -- mfhe_ctx creation: parameter validation and device table build.
+//
+// Table definitions (restating the reference's host-side setup):
+//   phantom NTT  -- phantom::arith::NTT(log_n, q) (PhantomContext at HE.cu:327-336)
+//   GL / cyclic  -- init_ntt_tables_manual + init_gl_twist_tables (ntt_core.cu:75-148, 175-198),
+//                   re-expressed for our CT network: root psi' = beta^2, twists beta^-j / beta^-2j
+//   GL perm      -- init_gl_perm_tables (ntt_core.cu:150-173)
+//   wide CRT     -- Encoder::Encoder CRT tables (encoder.cu:341-421), generalised to W words
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <cmath>
+#include <cstring>
+#include <string>
+#include <vector>
+
+#include "host_math.hpp"
+#include "mfhe_ctx.hpp"
+
+namespace mfhe {
+
+static thread_local std::string g_last_error;
+
+int set_error(int code, const std::string& msg) {
+    g_last_error = msg;
+    return code;
+}
+
+int hip_error(hipError_t e, const char* what) {
+    return set_error(MFHE_EHIP, std::string(what) + ": " + hipGetErrorString(e));
+}
+
+template <class T>
+static int dalloc(mfhe_ctx* c, T** p, size_t n) {
+    void* ptr = nullptr;
+    hipError_t e = hipMalloc(&ptr, std::max<size_t>(n, 1) * sizeof(T));
+    if (e != hipSuccess) return hip_error(e, "hipMalloc");
+    c->allocs.push_back(ptr);
+    *p = (T*)ptr;
+    return MFHE_OK;
+}
+
+template <class T>
+static int upload(mfhe_ctx* c, T** p, const std::vector<T>& h) {
+    int rc = dalloc(c, p, h.size());
+    if (rc) return rc;
+    MFHE_HIP(hipMemcpy(*p, h.data(), h.size() * sizeof(T), hipMemcpyHostToDevice));
+    return MFHE_OK;
+}
+
+static double centred(uint64_t w, uint64_t q) { return (w > q / 2) ? -(double)(q - w) : (double)w; }
+
+// Phantom-format table for root `psi` (order 2N): tw[brev(i)] = psi^i; itw[brev(i)] = psi^-i, itw[1] *= n^-1.
+static void build_ct_tables(uint64_t q, uint64_t psi, int logN, uint64_t* tw, uint64_t* itw, uint64_t* ninv) {
+    const uint32_t n = 1u << logN;
+    const uint64_t psi_inv = hm::invmod(psi, q);
+    uint64_t p = 1, pi = 1;
+    for (uint32_t i = 0; i < n; ++i) {
+        const uint32_t r = hm::brev(i, logN);
+        tw[r] = p;
+        itw[r] = pi;
+        p = hm::mulmod(p, psi, q);
+        pi = hm::mulmod(pi, psi_inv, q);
+    }
+    *ninv = hm::invmod(n % q, q);
+    if (n > 1) itw[1] = hm::mulmod(itw[1], *ninv, q);
+}
+
+struct HostTabs {
+    std::vector<uint64_t> tw, tws, itw, itws, ninv, ninvs;
+    std::vector<double2> twf, itwf, ninvf;
+};
+
+static void add_limb_tables(HostTabs& h, uint64_t q, uint64_t psi, int logN, bool f64) {
+    const size_t n = (size_t)1 << logN;
+    std::vector<uint64_t> tw(n), itw(n);
+    uint64_t ninv = 0;
+    build_ct_tables(q, psi, logN, tw.data(), itw.data(), &ninv);
+    for (size_t i = 0; i < n; ++i) {
+        h.tw.push_back(tw[i]);
+        h.tws.push_back(hm::shoup(tw[i], q));
+        h.itw.push_back(itw[i]);
+        h.itws.push_back(hm::shoup(itw[i], q));
+        if (f64) {
+            double a = centred(tw[i], q), b = centred(itw[i], q);
+            h.twf.push_back(make_double2(a, a / (double)q));
+            h.itwf.push_back(make_double2(b, b / (double)q));
+        }
+    }
+    h.ninv.push_back(ninv);
+    h.ninvs.push_back(hm::shoup(ninv, q));
+    if (f64) {
+        double a = centred(ninv, q);
+        h.ninvf.push_back(make_double2(a, a / (double)q));
+    }
+}
+
+static int upload_tabs(mfhe_ctx* c, HostTabs& h, NttTablesU& u, NttTablesF& f) {
+    int rc;
+    if ((rc = upload(c, &u.tw, h.tw)) || (rc = upload(c, &u.tws, h.tws)) || (rc = upload(c, &u.itw, h.itw)) ||
+        (rc = upload(c, &u.itws, h.itws)) || (rc = upload(c, &u.ninv, h.ninv)) || (rc = upload(c, &u.ninvs, h.ninvs)))
+        return rc;
+    if (!h.twf.empty()) {
+        if ((rc = upload(c, &f.tw, h.twf)) || (rc = upload(c, &f.itw, h.itwf)) || (rc = upload(c, &f.ninv, h.ninvf)))
+            return rc;
+    }
+    return MFHE_OK;
+}
+
+// powers table: out[j] = r^j, both u64 (+shoup) and F64 pairs
+static void powers(uint64_t q, uint64_t r, size_t n, bool f64, std::vector<uint64_t>& w, std::vector<uint64_t>& ws,
+                   std::vector<double2>& wf) {
+    uint64_t c = 1;
+    for (size_t j = 0; j < n; ++j) {
+        w.push_back(c);
+        ws.push_back(hm::shoup(c, q));
+        if (f64) {
+            double a = centred(c, q);
+            wf.push_back(make_double2(a, a / (double)q));
+        }
+        c = hm::mulmod(c, r, q);
+    }
+}
+
+static int build_crt(mfhe_ctx* c) {
+    const int L = c->L;
+    std::vector<uint64_t> Q(64, 0);
+    Q[0] = 1;
+    for (int i = 0; i < L; ++i) hm::big_mul_u64(Q.data(), c->moduli[i], Q.data(), 64);
+    const int W = std::max(1, (hm::bitlen(Q) + 1 + 63) / 64);
+    if (W > 32) return set_error(MFHE_EUNSUPPORTED, "wide CRT needs more than 32 words (product of moduli > 2^2047)");
+    c->W = W;
+    Q.resize(W);
+    std::vector<uint64_t> Qh(W), M((size_t)L * W), inv((size_t)L * 2), mu((size_t)L * 2);
+    std::vector<double> qinv(L);
+    uint64_t carry = 0;
+    for (int i = W - 1; i >= 0; --i) {
+        Qh[i] = (Q[i] >> 1) | (carry << 63);
+        carry = Q[i] & 1;
+    }
+    for (int k = 0; k < L; ++k) {
+        const uint64_t q = c->moduli[k];
+        hm::u128 rem = 0;
+        for (int i = W - 1; i >= 0; --i) {
+            hm::u128 cur = (rem << 64) | Q[i];
+            M[(size_t)k * W + i] = (uint64_t)(cur / q);
+            rem = cur % q;
+        }
+        hm::u128 r2 = 0;
+        for (int i = W - 1; i >= 0; --i) r2 = ((r2 << 64) | M[(size_t)k * W + i]) % q;
+        const uint64_t iv = hm::invmod((uint64_t)r2, q);
+        inv[2 * k] = iv;
+        inv[2 * k + 1] = hm::shoup(iv, q);
+        qinv[k] = 1.0 / (double)q;
+        mu[2 * k] = q;
+        mu[2 * k + 1] = (uint64_t)((((hm::u128)1) << 64) / q);
+    }
+    int rc;
+    if ((rc = upload(c, &c->d_crt_M, M)) || (rc = upload(c, &c->d_crt_inv, inv)) ||
+        (rc = upload(c, &c->d_crt_qinv, qinv)) || (rc = upload(c, &c->d_crt_Q, Q)) ||
+        (rc = upload(c, &c->d_crt_Qhalf, Qh)) || (rc = upload(c, &c->d_rns_mu, mu)))
+        return rc;
+    return MFHE_OK;
+}
+
+static int ctx_create_impl(const uint64_t* moduli, int L, int logN, int conv, double delta, mfhe_ctx** out) {
+    if (!out) return set_error(MFHE_EINVAL, "mfhe_ctx_create: out is null");
+    *out = nullptr;
+    if (!moduli || L < 1 || L > 256) return set_error(MFHE_EINVAL, "mfhe_ctx_create: need 1 <= L <= 256 moduli");
+    if (logN < 1 || logN > 17) return set_error(MFHE_EINVAL, "mfhe_ctx_create: log_n must be in [1, 17]");
+    if (!(delta > 0.0) || !std::isfinite(delta)) return set_error(MFHE_EINVAL, "mfhe_ctx_create: delta must be > 0");
+    const uint64_t N = 1ull << logN;
+    for (int i = 0; i < L; ++i) {
+        const uint64_t q = moduli[i];
+        if (q < 3 || q >= (1ull << 62) || !hm::is_prime(q))
+            return set_error(MFHE_EINVAL, "mfhe_ctx_create: modulus " + std::to_string(q) + " is not a prime < 2^62");
+        for (int j = 0; j < i; ++j)
+            if (moduli[j] == q) return set_error(MFHE_EINVAL, "mfhe_ctx_create: moduli must be distinct");
+        if ((conv & MFHE_CONV_PHANTOM) && (q - 1) % (2 * N) != 0)
+            return set_error(MFHE_EUNSUPPORTED, "modulus " + std::to_string(q) + " has no primitive 2N-th root");
+        if ((conv & MFHE_CONV_GL) && (q - 1) % (4 * N) != 0)
+            return set_error(MFHE_EUNSUPPORTED, "modulus " + std::to_string(q) + " has no primitive 4N-th root (GL)");
+        if ((conv & MFHE_CONV_WCRT) && (q - 1) % 771 != 0)
+            return set_error(MFHE_EUNSUPPORTED, "modulus " + std::to_string(q) + " has no 771-th root (W-CRT)");
+    }
+    mfhe_ctx* c = new mfhe_ctx();
+    c->L = L;
+    c->logN = logN;
+    c->N = N;
+    c->conv = conv;
+    c->delta = delta;
+    c->moduli.assign(moduli, moduli + L);
+    c->f64_ok = std::all_of(c->moduli.begin(), c->moduli.end(), [](uint64_t q) { return q < (1ull << 50); });
+    c->arith = c->f64_ok ? MFHE_ARITH_F64 : MFHE_ARITH_U64;
+    hipError_t he = hipGetDevice(&c->device);
+    int rc = MFHE_OK;
+    if (he != hipSuccess) rc = hip_error(he, "hipGetDevice");
+
+    auto fail = [&](int code) {
+        for (void* p : c->allocs) (void)hipFree(p);
+        delete c;
+        return code;
+    };
+    if (rc) return fail(rc);
+
+    // per-limb constants
+    std::vector<LimbConst> lcs(L);
+    std::vector<uint64_t> dmod((size_t)L * 3);
+    for (int i = 0; i < L; ++i) {
+        const uint64_t q = moduli[i];
+        lcs[i].q = q;
+        lcs[i].qf = (double)q;
+        lcs[i].qinv = 1.0 / (double)q;
+        lcs[i].pad = 0;
+        const hm::u128 two64 = ((hm::u128)1) << 64;
+        dmod[3 * i] = q;
+        dmod[3 * i + 2] = (uint64_t)(two64 / q);                          // high word of floor(2^128/q)
+        dmod[3 * i + 1] = (uint64_t)(((two64 % q) << 64) / q);           // low word
+    }
+    if ((rc = upload(c, &c->d_limbs, lcs)) || (rc = upload(c, &c->d_dmod, dmod))) return fail(rc);
+
+    if (conv & MFHE_CONV_PHANTOM) {
+        HostTabs h;
+        for (int i = 0; i < L; ++i) {
+            const uint64_t psi = hm::minimal_primitive_root(2 * N, moduli[i]);
+            if (!psi) return fail(set_error(MFHE_EUNSUPPORTED, "no primitive 2N-th root"));
+            add_limb_tables(h, moduli[i], psi, logN, c->f64_ok);
+        }
+        if ((rc = upload_tabs(c, h, c->ph_u, c->ph_f))) return fail(rc);
+    }
+    if (conv & MFHE_CONV_GL) {
+        HostTabs h;
+        std::vector<uint64_t> gpre, gpres, gpost, gposts, cpre, cpres, cpost, cposts;
+        std::vector<double2> gpref, gpostf, cpref, cpostf;
+        for (int i = 0; i < L; ++i) {
+            const uint64_t q = moduli[i];
+            const uint64_t beta = hm::first_psi4n(q, N);
+            if (!beta) return fail(set_error(MFHE_EUNSUPPORTED, "no psi4n (GL)"));
+            const uint64_t psi2 = hm::mulmod(beta, beta, q);   // primitive 2N-th root of the network
+            add_limb_tables(h, q, psi2, logN, c->f64_ok);
+            const uint64_t bi = hm::invmod(beta, q);
+            powers(q, bi, N, c->f64_ok, gpre, gpres, gpref);                     // beta^-j
+            powers(q, beta, N, c->f64_ok, gpost, gposts, gpostf);                // beta^j
+            powers(q, hm::mulmod(bi, bi, q), N, c->f64_ok, cpre, cpres, cpref);  // beta^-2j
+            powers(q, psi2, N, c->f64_ok, cpost, cposts, cpostf);                // beta^2j
+        }
+        if ((rc = upload_tabs(c, h, c->gl_u, c->gl_f))) return fail(rc);
+        if ((rc = upload(c, &c->gl_pre_u, gpre)) || (rc = upload(c, &c->gl_pre_us, gpres)) ||
+            (rc = upload(c, &c->gl_post_u, gpost)) || (rc = upload(c, &c->gl_post_us, gposts)) ||
+            (rc = upload(c, &c->cyc_pre_u, cpre)) || (rc = upload(c, &c->cyc_pre_us, cpres)) ||
+            (rc = upload(c, &c->cyc_post_u, cpost)) || (rc = upload(c, &c->cyc_post_us, cposts)))
+            return fail(rc);
+        if (c->f64_ok) {
+            if ((rc = upload(c, &c->gl_pre_f, gpref)) || (rc = upload(c, &c->gl_post_f, gpostf)) ||
+                (rc = upload(c, &c->cyc_pre_f, cpref)) || (rc = upload(c, &c->cyc_post_f, cpostf)))
+                return fail(rc);
+        }
+        // init_gl_perm_tables (ntt_core.cu:150-173)
+        std::vector<uint32_t> perm(N), iperm(N);
+        const uint32_t m = 4u * (uint32_t)N;
+        uint32_t e = 1 % m;
+        for (uint32_t j = 0; j < N; ++j) {
+            const uint32_t tgt = hm::brev((e - 1) / 4, logN);
+            perm[j] = tgt;
+            iperm[tgt] = j;
+            e = (uint32_t)((uint64_t)e * 5u % m);
+        }
+        if ((rc = upload(c, &c->gl_perm, perm)) || (rc = upload(c, &c->gl_inv_perm, iperm))) return fail(rc);
+    }
+    if ((rc = build_crt(c))) return fail(rc);
+    *out = c;
+    return MFHE_OK;
+}
+
+}  // namespace mfhe
+
+using namespace mfhe;
+
+extern "C" int mfhe_ctx_create(const uint64_t* moduli, int L, int log_n, int conventions, double delta,
+                               mfhe_ctx** out) {
+    try {
+        return ctx_create_impl(moduli, L, log_n, conventions, delta, out);
+    } catch (const std::exception& e) {
+        return set_error(MFHE_ENOMEM, std::string("mfhe_ctx_create: ") + e.what());
+    }
+}
+
+extern "C" int mfhe_ctx_destroy(mfhe_ctx* c) {
+    if (!c) return MFHE_OK;
+    for (void* p : c->allocs) (void)hipFree(p);
+    delete c;
+    return MFHE_OK;
+}
+
+extern "C" int mfhe_ctx_get_info(const mfhe_ctx* c, mfhe_ctx_info* info) {
+    if (!c || !info) return set_error(MFHE_EINVAL, "mfhe_ctx_get_info: null argument");
+    info->num_limbs = c->L;
+    info->log_n = c->logN;
+    info->crt_words = c->W;
+    info->arith = c->arith;
+    info->conventions = c->conv;
+    info->phi = (c->conv & MFHE_CONV_WCRT) ? 512 : 0;
+    info->delta = c->delta;
+    return MFHE_OK;
+}
+
+extern "C" int mfhe_ctx_set_arith(mfhe_ctx* c, int arith) {
+    if (!c) return set_error(MFHE_EINVAL, "mfhe_ctx_set_arith: null ctx");
+    if (arith == MFHE_ARITH_AUTO) arith = c->f64_ok ? MFHE_ARITH_F64 : MFHE_ARITH_U64;
+    if (arith == MFHE_ARITH_F64 && !c->f64_ok)
+        return set_error(MFHE_EUNSUPPORTED, "F64 arithmetic needs every modulus < 2^50");
+    if (arith != MFHE_ARITH_F64 && arith != MFHE_ARITH_U64) return set_error(MFHE_EINVAL, "bad arith");
+    c->arith = arith;
+    return MFHE_OK;
+}
+
+extern "C" int mfhe_ctx_get_moduli(const mfhe_ctx* c, uint64_t* out, int count) {
+    if (!c || !out || count < c->L) return set_error(MFHE_EINVAL, "mfhe_ctx_get_moduli: bad argument");
+    std::memcpy(out, c->moduli.data(), (size_t)c->L * 8);
+    return MFHE_OK;
+}
+
+extern "C" const char* mfhe_last_error(void) { return g_last_error.c_str(); }
+extern "C" const char* mfhe_version(void) { return "mfhe-mi355x 0.1 (gfx950)"; }

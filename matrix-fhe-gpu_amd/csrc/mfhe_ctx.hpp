@@ -1,0 +1,86 @@
+// mfhe_ctx.hpp -- internal definition of the context object behind include/mfhe.h.
+//
+// One context = one parameter set on one device: moduli, ring degree N, scale,
+// and every device table the hot path needs, built once at create time
+// (the reference rebuilds/re-uploads tables lazily from many places and
+// keys them on the first caller's limb count).
+#pragma once
+#include <hip/hip_runtime.h>
+
+#include <cstdint>
+#include <string>
+#include <vector>
+
+#include "../../include/mfhe.h"
+#include "ntt_arith.hpp"
+
+namespace mfhe {
+
+// thread-local error reporting
+int set_error(int code, const std::string& msg);
+int hip_error(hipError_t e, const char* what);
+
+#define MFHE_HIP(call)                                          \
+    do {                                                        \
+        hipError_t _e = (call);                                 \
+        if (_e != hipSuccess) return ::mfhe::hip_error(_e, #call); \
+    } while (0)
+
+#define MFHE_CHECK_LAUNCH(what)                                 \
+    do {                                                        \
+        hipError_t _e = hipGetLastError();                      \
+        if (_e != hipSuccess) return ::mfhe::hip_error(_e, what); \
+    } while (0)
+
+struct NttTablesF {   // FP64 path: (w centred, w/q) pairs
+    double2* tw = nullptr;    // [L][N]
+    double2* itw = nullptr;   // [L][N], itw[1] *= n^-1
+    double2* ninv = nullptr;  // [L]
+};
+struct NttTablesU {   // U64 path / phantom format
+    uint64_t* tw = nullptr;     // [L][N]
+    uint64_t* tws = nullptr;
+    uint64_t* itw = nullptr;
+    uint64_t* itws = nullptr;
+    uint64_t* ninv = nullptr;   // [L]
+    uint64_t* ninvs = nullptr;
+};
+
+}  // namespace mfhe
+
+struct mfhe_ctx {
+    int L = 0;
+    int logN = 0;
+    uint64_t N = 0;
+    int conv = 0;
+    int arith = MFHE_ARITH_AUTO;  // effective: F64 or U64
+    bool f64_ok = false;          // every q < 2^50
+    double delta = 0.0;
+    int device = 0;
+    std::vector<uint64_t> moduli;
+
+    mfhe::LimbConst* d_limbs = nullptr;  // [L]
+    uint64_t* d_dmod = nullptr;          // [L][3] phantom DModulus {value, const_ratio[2]}
+
+    // phantom convention tables (psi = minimal primitive 2N-th root)
+    mfhe::NttTablesF ph_f;
+    mfhe::NttTablesU ph_u;
+    // GL / cyclic tables (network root psi' = beta^2, beta = first-found psi4n)
+    mfhe::NttTablesF gl_f;
+    mfhe::NttTablesU gl_u;
+    double2 *gl_pre_f = nullptr, *gl_post_f = nullptr, *cyc_pre_f = nullptr, *cyc_post_f = nullptr;  // [L][N]
+    uint64_t *gl_pre_u = nullptr, *gl_pre_us = nullptr, *gl_post_u = nullptr, *gl_post_us = nullptr;
+    uint64_t *cyc_pre_u = nullptr, *cyc_pre_us = nullptr, *cyc_post_u = nullptr, *cyc_post_us = nullptr;
+    uint32_t *gl_perm = nullptr, *gl_inv_perm = nullptr;  // [N]
+
+    // wide CRT tables (encoder.cu:341-421), W words
+    int W = 0;
+    uint64_t* d_crt_M = nullptr;      // [L][W]  M_k = Q / q_k
+    uint64_t* d_crt_inv = nullptr;    // [L][2]  (inv_k, shoup(inv_k))
+    double* d_crt_qinv = nullptr;     // [L]     1/q_k (quotient estimate)
+    uint64_t* d_crt_Q = nullptr;      // [W]
+    uint64_t* d_crt_Qhalf = nullptr;  // [W]
+    uint64_t* d_rns_mu = nullptr;     // [L][2] (q, floor(2^64/q))
+
+    std::vector<void*> allocs;  // everything above, freed at destroy
+};

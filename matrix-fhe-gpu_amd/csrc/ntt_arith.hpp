@@ -1,0 +1,126 @@
+// ntt_arith.hpp -- modular arithmetic policies for the CDNA4 NTT kernels.
+//
+// Two interchangeable policies drive the same butterfly network:
+//
+//  * ArithF64 -- residues held as exact integers in IEEE doubles (q < 2^50).
+//    A modmul is an error-free transformation: hi = v*w, lo = fma(v,w,-hi),
+//    k = rint(v*w/q), t = fma(-k,q,hi) + lo.  Every step is exact while
+//    |values| < 2^53, which the reduction schedule guarantees (DESIGN.md
+//    §Arithmetic).  Measured on gfx950: 2.1e12 butterflies/s vs 1.3e12 for the
+//    64-bit integer Shoup butterfly (profiles/r01_microbench_modmul.txt).
+//
+//  * ArithU64 -- Harvey lazy butterflies with Shoup precomputation, exactly the
+//    phantom fnwt/inwt arithmetic: values in [0,4q), q < 2^62.
+//    Used when any modulus is >= 2^50 and for the phantom fnwt_1d/inwt_1d surface,
+//    whose callers hand us u64 Shoup tables.
+//
+// Both produce canonical [0,q) outputs, so results are bit-identical to each
+// other and to the phantom/reference transforms they restate.
+#pragma once
+#include <hip/hip_runtime.h>
+#include <cstdint>
+
+namespace mfhe {
+
+constexpr double kTwo52 = 4503599627370496.0;          // 2^52
+constexpr uint64_t kExp52 = 0x4330000000000000ULL;      // bits of 2^52
+
+// Per-limb constants passed to kernels.
+struct LimbConst {
+    uint64_t q;
+    double qf, qinv;
+    uint64_t pad;
+};
+
+struct ArithF64 {
+    using T = double;
+    using Tw = double2;      // (w, w/q), w centred in (-q/2, q/2]
+    double q, qinv;
+
+    __device__ __forceinline__ explicit ArithF64(const LimbConst& c) : q(c.qf), qinv(c.qinv) {}
+
+    // canonical u64 (< 2^52) -> exact double
+    __device__ __forceinline__ static double from_u64(uint64_t x) {
+        return __longlong_as_double((long long)(x | kExp52)) - kTwo52;
+    }
+    // intermediate representation between passes: raw double bits
+    __device__ __forceinline__ static double from_raw(uint64_t x) { return __longlong_as_double((long long)x); }
+    __device__ __forceinline__ static uint64_t to_raw(double x) { return (uint64_t)__double_as_longlong(x); }
+
+    // t = v*w mod q, |t| <= q/2 + |v||w| 2^-53 (exact integer in a double)
+    __device__ __forceinline__ double mulmod(double v, Tw w) const {
+        double hi = v * w.x;
+        double lo = __fma_rn(v, w.x, -hi);
+        double k = __builtin_rint(v * w.y);
+        return __fma_rn(-k, q, hi) + lo;
+    }
+    // centred reduction: |result| <= q/2 (+ negligible) for |x| < 2^53
+    __device__ __forceinline__ double reduce(double x) const {
+        return __fma_rn(-__builtin_rint(x * qinv), q, x);
+    }
+    // Cooley-Tukey: (u, v) <- (u + wv, u - wv)
+    __device__ __forceinline__ void ct(double& u, double& v, Tw w) const {
+        double t = mulmod(v, w);
+        double a = u;
+        u = a + t;
+        v = a - t;
+    }
+    // Gentleman-Sande: (u, v) <- (u + v, (u - v) w); X re-reduced (it doubles per stage)
+    __device__ __forceinline__ void gs(double& u, double& v, Tw w) const {
+        double a = u, b = v;
+        u = reduce(a + b);
+        v = mulmod(a - b, w);
+    }
+    // start-of-round reduction (keeps CT growth bounded)
+    __device__ __forceinline__ double round_reduce(double x) const { return reduce(x); }
+    // exact canonical u64 in [0, q)
+    __device__ __forceinline__ uint64_t canon(double x) const {
+        double k = __builtin_floor(x * qinv);
+        double r = __fma_rn(-k, q, x);
+        r = (r < 0.0) ? r + q : r;
+        r = (r >= q) ? r - q : r;
+        return (uint64_t)__double_as_longlong(r + kTwo52) & 0x000FFFFFFFFFFFFFULL;
+    }
+};
+
+struct ArithU64 {
+    using T = uint64_t;
+    using Tw = ulonglong2;   // (w, floor(w 2^64 / q))
+    uint64_t q, two_q;
+
+    __device__ __forceinline__ explicit ArithU64(const LimbConst& c) : q(c.q), two_q(2 * c.q) {}
+
+    __device__ __forceinline__ static uint64_t from_u64(uint64_t x) { return x; }
+    __device__ __forceinline__ static uint64_t from_raw(uint64_t x) { return x; }
+    __device__ __forceinline__ static uint64_t to_raw(uint64_t x) { return x; }
+
+    // Shoup: v*w - hi64(v*w')*q in [0, 2q) for any v < 2^64
+    __device__ __forceinline__ uint64_t mulmod(uint64_t v, Tw w) const {
+        return v * w.x - __umul64hi(v, w.y) * q;
+    }
+    __device__ __forceinline__ uint64_t reduce(uint64_t x) const {   // [0,4q) -> [0,2q)
+        return (x >= two_q) ? x - two_q : x;
+    }
+    // Harvey CT: u in [0,4q), v < 2^64 -> outputs in [0,4q)
+    __device__ __forceinline__ void ct(uint64_t& u, uint64_t& v, Tw w) const {
+        uint64_t t = mulmod(v, w);
+        uint64_t a = reduce(u);
+        u = a + t;
+        v = a - t + two_q;
+    }
+    // Harvey GS: u, v in [0,2q) -> outputs in [0,2q)
+    __device__ __forceinline__ void gs(uint64_t& u, uint64_t& v, Tw w) const {
+        uint64_t a = u, b = v;
+        u = reduce(a + b);
+        v = mulmod(a - b + two_q, w);
+    }
+    __device__ __forceinline__ uint64_t round_reduce(uint64_t x) const { return x; }
+    __device__ __forceinline__ uint64_t canon(uint64_t x) const {
+        x = (x >= two_q) ? x - two_q : x;
+        return (x >= q) ? x - q : x;
+    }
+};
+
+
+
+}  // namespace mfhe

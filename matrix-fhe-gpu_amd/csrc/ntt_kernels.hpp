@@ -1,0 +1,250 @@
+// ntt_kernels.hpp -- batched NTT pass kernels for gfx950 (CDNA4).
+//
+// Transform: the phantom-fhe negacyclic NTT (SEAL convention) restated in
+// SURVEY.md Appendix A -- Cooley-Tukey forward with tw[m+i] = psi^brev(m+i),
+// bit-reversed output; Gentleman-Sande inverse with itw[m+i] = psi^-brev(m+i),
+// n^-1 folded into the last stage.  Reference call sites: ntt_core.cu:443-460
+// (xy_ntt_forward/backward_phantom -> fnwt_1d/inwt_1d).
+//
+// Decomposition.  Stage s (0..logN-1) pairs elements j, j + N/2^(s+1).  A
+// *pass* runs stages [s0, s0+LOG_G) on independent *groups* of G = 2^LOG_G
+// elements: for fixed (hi, lo) the group is j = hi<<(logN-s0) | g<<logS | lo,
+// g in [0,G), S = 2^logS = N / 2^(s0+LOG_G).  Inside a pass each thread holds
+// R = 2^LOG_R elements in registers and runs up to LOG_R stages per *round*;
+// rounds exchange data through padded LDS.  N <= 2^14 runs as one pass (whole
+// polynomial per workgroup); N = 2^15..2^17 as two passes (column pass with
+// coalesced strided groups, then contiguous-block pass).
+//
+// Lane maps.  COLS (strided groups, S >= NG): lane -> group first, so every
+// wave instruction touches NG consecutive columns; any g-layout is coalesced.
+// Block mode (contiguous groups): lane -> tau first; only the round-0 layout
+// (g = tau + TG*k) is coalesced, so loads/stores go through that layout.
+//
+// Workgroup -> data mapping is XCD aware: hardware deals blocks round-robin
+// over the 8 XCDs, we remap so each XCD walks a contiguous range of a
+// limb-major ordering, keeping one limb's twiddle table hot in that XCD's L2.
+#pragma once
+#include <type_traits>
+
+#include "ntt_arith.hpp"
+
+namespace mfhe {
+
+struct TwSrcF {
+    const double2* p;
+    __device__ __forceinline__ double2 get(size_t i) const { return p[i]; }
+};
+struct TwSrcU {
+    const uint64_t* w;
+    const uint64_t* ws;
+    __device__ __forceinline__ ulonglong2 get(size_t i) const { return make_ulonglong2(w[i], ws[i]); }
+};
+
+template <class TS>
+struct PassArgs {
+    uint64_t* data;          // [batch][nl][N]
+    TS tw;                   // [mod][N]  (forward or inverse table)
+    TS twist;                // [mod][N]  pre-twist (fwd) / post-twist (inv), TWIST only
+    TS ninv;                 // [mod]     inverse last-stage X scale (n^-1)
+    const LimbConst* limbs;  // [mod]; null -> q read from qraw[mod * qstride] (phantom DModulus)
+    const uint64_t* qraw;
+    int qstride;
+    uint64_t batch;
+    int nl, start_limb;
+    int logN, s0;
+    uint32_t nblocks;
+};
+
+__device__ __forceinline__ uint32_t xcd_remap(uint32_t b, uint32_t nb) {
+    const uint32_t q = nb >> 3, r = nb & 7, x = b & 7, s = b >> 3;
+    return (x < r ? x * (q + 1) : r * (q + 1) + (x - r) * q) + s;
+}
+
+template <int LOG_G, int LOG_R>
+struct Geo {
+    static constexpr int G = 1 << LOG_G;
+    static constexpr int R = 1 << LOG_R;
+    static constexpr int TG = G / R;
+    static constexpr int NR = (LOG_G + LOG_R - 1) / LOG_R;
+    static constexpr int GS = G + G / 16 + 1;   // odd padded group stride (doubles)
+    __host__ __device__ static constexpr int HB(int r) { return LOG_G - 1 - r * LOG_R; }
+    __host__ __device__ static constexpr int WL(int r) { return (HB(r) - LOG_R + 1) > 0 ? (HB(r) - LOG_R + 1) : 0; }
+    __device__ __forceinline__ static uint32_t g_of(int r, uint32_t tau, uint32_t k) {
+        const int wl = WL(r);
+        return ((tau >> wl) << (wl + LOG_R)) | (k << wl) | (tau & ((1u << wl) - 1));
+    }
+    __device__ __forceinline__ static uint32_t pad(uint32_t g) { return g + (g >> 4); }
+};
+
+__device__ __forceinline__ uint32_t brev_bits(uint32_t x, int bits) { return __brev(x) >> (32 - bits); }
+
+template <int I, int N, class F>
+__device__ __forceinline__ void static_for(F&& f) {
+    if constexpr (I < N) {
+        f(std::integral_constant<int, I>{});
+        static_for<I + 1, N>(f);
+    }
+}
+
+template <class A, class TS, int LOG_G, int LOG_R, int NG, bool COLS, bool INV, bool IN_RAW, bool OUT_RAW,
+          bool TWIST, bool BREV>
+__global__ __launch_bounds__(NG * (1 << (LOG_G - LOG_R))) void ntt_pass_kernel(PassArgs<TS> a) {
+    using Gm = Geo<LOG_G, LOG_R>;
+    using T = typename A::T;
+    using Tw = typename A::Tw;
+    constexpr int R = Gm::R, TG = Gm::TG, NR = Gm::NR, GS = Gm::GS;
+    extern __shared__ __attribute__((aligned(16))) uint64_t lds[];
+
+    const uint32_t t = threadIdx.x;
+    const uint32_t gl = COLS ? (t % NG) : (t / TG);
+    const uint32_t tau = COLS ? (t / NG) : (t % TG);
+
+    const int logN = a.logN;
+    const int logS = logN - a.s0 - LOG_G;
+    const uint64_t S = 1ull << logS;
+    const uint64_t gpp = S << a.s0;  // groups per polynomial-limb
+    const uint64_t npl = a.batch * (uint64_t)a.nl;
+    const uint32_t lb = xcd_remap(blockIdx.x, a.nblocks);
+
+    uint64_t v, hi, lo;
+    if constexpr (COLS) {
+        const uint64_t tpp = gpp / NG, cols_tiles = S / NG;
+        v = lb / tpp;
+        const uint64_t tile = lb % tpp;
+        hi = tile / cols_tiles;
+        lo = (tile % cols_tiles) * NG + gl;
+    } else {
+        const uint64_t gid = (uint64_t)lb * NG + gl;
+        v = gid / gpp;
+        const uint64_t rem = gid % gpp;
+        hi = rem >> logS;
+        lo = rem & (S - 1);
+    }
+    const bool active = v < npl;
+    if (!active) v = 0;
+    // virtual poly index is limb-major: v = l * batch + b
+    const int l = (int)(v / a.batch);
+    const uint64_t b = v % a.batch;
+    const int mod = a.start_limb + l;
+    const uint64_t N = 1ull << logN;
+    uint64_t* base = a.data + (b * (uint64_t)a.nl + (uint64_t)l) * N;
+    const size_t twoff = (size_t)mod * N;
+    LimbConst lc;
+    if (a.limbs) {
+        lc = a.limbs[mod];
+    } else {
+        lc.q = a.qraw[(size_t)mod * a.qstride];
+        lc.qf = (double)lc.q;
+        lc.qinv = 1.0 / lc.qf;
+    }
+    const A ar(lc);
+
+    const uint64_t jhi = hi << (logN - a.s0);
+    auto jidx = [&](uint32_t g) -> uint64_t { return jhi | ((uint64_t)g << logS) | lo; };
+
+    T x[R];
+    uint64_t* my_lds = lds + (size_t)gl * GS;
+
+    auto exchange = [&](auto rf, auto rt, bool brev_pos) {
+        constexpr int r_from = decltype(rf)::value, r_to = decltype(rt)::value;
+        __syncthreads();
+#pragma unroll
+        for (int k = 0; k < R; ++k) {
+            uint32_t g = Gm::g_of(r_from, tau, k);
+            if (brev_pos) g = brev_bits(g, LOG_G);
+            my_lds[Gm::pad(g)] = A::to_raw(x[k]);
+        }
+        __syncthreads();
+#pragma unroll
+        for (int k = 0; k < R; ++k) x[k] = A::from_raw(my_lds[Gm::pad(Gm::g_of(r_to, tau, k))]);
+    };
+
+    // ---- load ----
+    constexpr int r_load = (INV && COLS) ? (NR - 1) : 0;
+#pragma unroll
+    for (int k = 0; k < R; ++k) {
+        const uint32_t g = Gm::g_of(r_load, tau, k);
+        const uint64_t raw = active ? base[jidx(g)] : 0;
+        x[k] = IN_RAW ? A::from_raw(raw) : A::from_u64(raw);
+        if constexpr (TWIST && !INV) x[k] = ar.mulmod(x[k], a.twist.get(twoff + jidx(g)));
+    }
+    if constexpr (INV && !COLS && (NR > 1 || BREV))
+        exchange(std::integral_constant<int, 0>{}, std::integral_constant<int, NR - 1>{}, BREV);
+
+    // ---- one stage on register bit bb of round r ----
+    auto stage = [&](auto rc, auto bc) {
+        constexpr int r = decltype(rc)::value, bb = decltype(bc)::value;
+        constexpr int hb = Gm::HB(r), wl = Gm::WL(r);
+        constexpr int bit = wl + bb;
+        if constexpr (bit <= hb) {
+            const int s = a.s0 + (LOG_G - 1 - bit);
+            constexpr int half = 1 << bb;
+            const uint64_t tau_hi = tau >> wl;
+            const uint64_t twb = twoff + (1ull << s) + (hi << (LOG_G - 1 - bit)) + (tau_hi << (LOG_R - 1 - bb));
+            if constexpr (!INV) {
+#pragma unroll
+                for (int k = 0; k < R; ++k) {
+                    if (k & half) continue;
+                    const Tw w = a.tw.get(twb + (uint64_t)(k >> (bb + 1)));
+                    ar.ct(x[k], x[k + half], w);
+                }
+            } else {
+                if (s == 0) {
+                    const Tw wn = a.ninv.get((size_t)mod);
+                    const Tw w1 = a.tw.get(twoff + 1);
+#pragma unroll
+                    for (int k = 0; k < R; ++k) {
+                        if (k & half) continue;
+                        T u = x[k], vv = x[k + half];
+                        ar.gs(u, vv, w1);          // u = red(u+v), vv = (u-v) * itw[1]
+                        x[k] = ar.mulmod(u, wn);   // X * n^-1
+                        x[k + half] = vv;
+                    }
+                } else {
+#pragma unroll
+                    for (int k = 0; k < R; ++k) {
+                        if (k & half) continue;
+                        const Tw w = a.tw.get(twb + (uint64_t)(k >> (bb + 1)));
+                        ar.gs(x[k], x[k + half], w);
+                    }
+                }
+            }
+        }
+    };
+
+    if constexpr (!INV) {
+        static_for<0, NR>([&](auto rc) {
+            constexpr int r = decltype(rc)::value;
+            if constexpr (r > 0) {
+                exchange(std::integral_constant<int, r - 1>{}, rc, false);
+#pragma unroll
+                for (int k = 0; k < R; ++k) x[k] = ar.round_reduce(x[k]);
+            }
+            static_for<0, LOG_R>([&](auto bi) {
+                stage(rc, std::integral_constant<int, LOG_R - 1 - decltype(bi)::value>{});
+            });
+        });
+    } else {
+        static_for<0, NR>([&](auto ri) {
+            constexpr int r = NR - 1 - decltype(ri)::value;
+            if constexpr (r < NR - 1) exchange(std::integral_constant<int, r + 1>{}, std::integral_constant<int, r>{}, false);
+            static_for<0, LOG_R>([&](auto bi) { stage(std::integral_constant<int, r>{}, bi); });
+        });
+    }
+
+    // ---- store ----
+    constexpr int r_store = (!INV && COLS) ? (NR - 1) : 0;
+    if constexpr (!INV && !COLS && (NR > 1 || BREV))
+        exchange(std::integral_constant<int, NR - 1>{}, std::integral_constant<int, 0>{}, BREV);
+    if (active) {
+#pragma unroll
+        for (int k = 0; k < R; ++k) {
+            const uint32_t g = Gm::g_of(r_store, tau, k);
+            T y = x[k];
+            if constexpr (TWIST && INV) y = ar.mulmod(y, a.twist.get(twoff + jidx(g)));
+            base[jidx(g)] = OUT_RAW ? A::to_raw(ar.reduce(y)) : ar.canon(y);
+        }
+    }
+}
+
+}  // namespace mfhe

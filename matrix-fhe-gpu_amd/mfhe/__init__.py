@@ -1,0 +1,249 @@
+"""mfhe -- Python host layer over libmfhe.so (include/mfhe.h), the MI355X backend for the
+Matrix-FHE-GPU hot path (batched NTT/INTT, wide RNS CRT encode/decode).
+
+The reference exposes this path through C++ (include/core/*.cuh) and phantom-fhe; this
+module mirrors that surface for tests and benchmarks.  PyTorch is used only for device
+memory and streams: every tensor is handed to the native library as a raw pointer.
+There is no CPU or PyTorch fallback -- if libmfhe.so is missing or fails to load, import
+raises.
+"""
+from __future__ import annotations
+
+import ctypes
+import os
+import re
+from pathlib import Path
+
+_PKG_DIR = Path(__file__).resolve().parent.parent          # matrix-fhe-gpu_amd/
+REPO_ROOT = _PKG_DIR.parent
+LIB_PATH = _PKG_DIR / "libmfhe.so"
+HEADER = REPO_ROOT / "include" / "mfhe.h"
+
+OK, EINVAL, EUNSUPPORTED, EHIP, ENOMEM, ENOTREADY = 0, 1, 2, 3, 4, 5
+CONV_PHANTOM, CONV_GL, CONV_WCRT = 1, 2, 4
+ARITH_AUTO, ARITH_F64, ARITH_U64 = 0, 1, 2
+
+#: reference parameters (include/core/config.h:7-52)
+RNS_MODULI = [
+    17592186435073, 17182765057, 17184541441, 17186120449, 17186515201, 17186909953,
+    17188883713, 17190462721, 17190857473, 17191844353, 17192831233,
+]
+P_MODULI = [18014398515156481, 549757491457, 549759662593]
+MATRIX_N = 64
+BATCH_SIZE = 512
+BATCH_PRIME_P = 771
+SCALING_FACTOR = 2.0 ** 35
+
+
+class MfheError(RuntimeError):
+    def __init__(self, code: int, msg: str):
+        super().__init__(f"mfhe error {code}: {msg}")
+        self.code = code
+
+
+def _load() -> ctypes.CDLL:
+    if not LIB_PATH.exists():
+        raise ImportError(f"{LIB_PATH} not built; run `make -C {_PKG_DIR}` (or __graft_entry__.build())")
+    return ctypes.CDLL(str(LIB_PATH), mode=ctypes.RTLD_GLOBAL)
+
+
+lib = _load()
+
+_u64p = ctypes.POINTER(ctypes.c_uint64)
+_vp = ctypes.c_void_p
+_sz = ctypes.c_size_t
+
+
+class CtxInfo(ctypes.Structure):
+    _fields_ = [
+        ("num_limbs", ctypes.c_int), ("log_n", ctypes.c_int), ("crt_words", ctypes.c_int),
+        ("arith", ctypes.c_int), ("conventions", ctypes.c_int), ("phi", ctypes.c_int),
+        ("delta", ctypes.c_double),
+    ]
+
+
+def _sig(name, argtypes, restype=ctypes.c_int):
+    f = getattr(lib, name)
+    f.argtypes = argtypes
+    f.restype = restype
+    return f
+
+
+_sig("mfhe_ctx_create", [_u64p, ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_double, ctypes.POINTER(_vp)])
+_sig("mfhe_ctx_destroy", [_vp])
+_sig("mfhe_ctx_get_info", [_vp, ctypes.POINTER(CtxInfo)])
+_sig("mfhe_ctx_set_arith", [_vp, ctypes.c_int])
+_sig("mfhe_ctx_get_moduli", [_vp, _u64p, ctypes.c_int])
+for _n in ("mfhe_ntt_fwd", "mfhe_ntt_inv", "mfhe_gl_ntt_fwd", "mfhe_gl_ntt_inv", "mfhe_cyclic_ntt_fwd",
+           "mfhe_cyclic_ntt_inv"):
+    _sig(_n, [_vp, _vp, _sz, ctypes.c_int, ctypes.c_int, _vp])
+_sig("mfhe_gl_perm", [_vp, _vp, _vp, _sz, ctypes.c_int, ctypes.c_int, _vp])
+_sig("mfhe_ntt_tables", [_vp] + [ctypes.POINTER(_vp)] * 6)
+_sig("mfhe_ntt_dmodulus", [_vp, ctypes.POINTER(_vp)])
+_sig("mfhe_fnwt_1d", [_vp, _vp, _vp, _vp, _sz, _sz, _sz, _sz, _vp])
+_sig("mfhe_inwt_1d", [_vp, _vp, _vp, _vp, _vp, _vp, _sz, _sz, _sz, _sz, _vp])
+_sig("mfhe_rns_decompose", [_vp, _vp, _sz, _sz, _sz, _vp, _vp])
+_sig("mfhe_crt_compose", [_vp, _vp, _sz, _sz, _vp, _vp, _vp])
+_sig("mfhe_crt_to_f64", [_vp, _vp, _vp, _sz, _vp, _sz, _vp])
+_sig("mfhe_crt_compose_f64", [_vp, _vp, _sz, _sz, _vp, _sz, _vp])
+_sig("mfhe_last_error", [], ctypes.c_char_p)
+_sig("mfhe_version", [], ctypes.c_char_p)
+
+
+def declared_symbols(header: Path = None) -> list[str]:
+    """Every function name declared in include/*.h (the C-ABI surface)."""
+    hdrs = [header] if header else sorted((REPO_ROOT / "include").glob("*.h"))
+    names = []
+    for h in hdrs:
+        text = re.sub(r"/\*.*?\*/", "", h.read_text(), flags=re.S)
+        names += re.findall(r"\b(mfhe_[a-z0-9_]+)\s*\(", text)
+    return sorted(set(names))
+
+
+def check(rc: int, what: str = "") -> None:
+    if rc != OK:
+        raise MfheError(rc, f"{what}: {lib.mfhe_last_error().decode()}")
+
+
+def _stream_ptr(stream) -> int:
+    import torch
+    s = stream if stream is not None else torch.cuda.current_stream()
+    return s.cuda_stream
+
+
+def _ptr(t) -> int:
+    if t is None:
+        return None
+    if not t.is_cuda:
+        raise ValueError("mfhe operates on device tensors")
+    if not t.is_contiguous():
+        raise ValueError("mfhe needs contiguous tensors")
+    return t.data_ptr()
+
+
+class Context:
+    """One parameter set + device tables (mfhe_ctx).  Mirrors init_he_backend /
+    PhantomContext / Encoder table setup of the reference."""
+
+    def __init__(self, moduli, log_n: int, conventions: int = CONV_PHANTOM, delta: float = SCALING_FACTOR):
+        arr = (ctypes.c_uint64 * len(moduli))(*[int(m) for m in moduli])
+        h = _vp()
+        check(lib.mfhe_ctx_create(arr, len(moduli), int(log_n), int(conventions), float(delta), ctypes.byref(h)),
+              "mfhe_ctx_create")
+        self._h = h
+        self.moduli = [int(m) for m in moduli]
+        self.L = len(self.moduli)
+        self.log_n = int(log_n)
+        self.N = 1 << self.log_n
+        self.delta = float(delta)
+        info = self.info()
+        self.crt_words = info.crt_words
+        self.phi = info.phi
+
+    @property
+    def handle(self):
+        return self._h
+
+    def info(self) -> CtxInfo:
+        inf = CtxInfo()
+        check(lib.mfhe_ctx_get_info(self._h, ctypes.byref(inf)), "get_info")
+        return inf
+
+    def set_arith(self, arith: int) -> None:
+        check(lib.mfhe_ctx_set_arith(self._h, arith), "set_arith")
+
+    def close(self):
+        if getattr(self, "_h", None):
+            lib.mfhe_ctx_destroy(self._h)
+            self._h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    # ---- NTT ----
+    def _ntt(self, fn, data, batch, start_limb, nlimbs, stream):
+        nl = self.L - start_limb if nlimbs is None else nlimbs
+        if batch is None:
+            batch = data.numel() // (nl * self.N)
+        if data.numel() < batch * nl * self.N:
+            raise ValueError("tensor smaller than batch * nlimbs * N")
+        check(fn(self._h, _ptr(data), batch, start_limb, nl, _stream_ptr(stream)), fn.__name__)
+        return data
+
+    def ntt_fwd(self, data, batch=None, start_limb=0, nlimbs=None, stream=None):
+        return self._ntt(lib.mfhe_ntt_fwd, data, batch, start_limb, nlimbs, stream)
+
+    def ntt_inv(self, data, batch=None, start_limb=0, nlimbs=None, stream=None):
+        return self._ntt(lib.mfhe_ntt_inv, data, batch, start_limb, nlimbs, stream)
+
+    def gl_ntt_fwd(self, data, batch=None, start_limb=0, nlimbs=None, stream=None):
+        return self._ntt(lib.mfhe_gl_ntt_fwd, data, batch, start_limb, nlimbs, stream)
+
+    def gl_ntt_inv(self, data, batch=None, start_limb=0, nlimbs=None, stream=None):
+        return self._ntt(lib.mfhe_gl_ntt_inv, data, batch, start_limb, nlimbs, stream)
+
+    def cyclic_ntt_fwd(self, data, batch=None, start_limb=0, nlimbs=None, stream=None):
+        return self._ntt(lib.mfhe_cyclic_ntt_fwd, data, batch, start_limb, nlimbs, stream)
+
+    def cyclic_ntt_inv(self, data, batch=None, start_limb=0, nlimbs=None, stream=None):
+        return self._ntt(lib.mfhe_cyclic_ntt_inv, data, batch, start_limb, nlimbs, stream)
+
+    def gl_perm(self, src, dst, batch, nlimbs=None, inverse=False, stream=None):
+        nl = self.L if nlimbs is None else nlimbs
+        check(lib.mfhe_gl_perm(self._h, _ptr(src), _ptr(dst), batch, nl, int(inverse), _stream_ptr(stream)), "gl_perm")
+        return dst
+
+    def ntt_tables(self):
+        ps = [_vp() for _ in range(6)]
+        check(lib.mfhe_ntt_tables(self._h, *[ctypes.byref(p) for p in ps]), "ntt_tables")
+        dm = _vp()
+        check(lib.mfhe_ntt_dmodulus(self._h, ctypes.byref(dm)), "ntt_dmodulus")
+        return [p.value for p in ps] + [dm.value]
+
+    # ---- wide CRT ----
+    def rns_decompose(self, src, dst, npoly, ncoeff, in_stride=1, stream=None):
+        check(lib.mfhe_rns_decompose(self._h, _ptr(src), in_stride, npoly, ncoeff, _ptr(dst), _stream_ptr(stream)),
+              "rns_decompose")
+        return dst
+
+    def crt_compose(self, src, mag, neg, npoly, ncoeff, stream=None):
+        check(lib.mfhe_crt_compose(self._h, _ptr(src), npoly, ncoeff, _ptr(mag), _ptr(neg), _stream_ptr(stream)),
+              "crt_compose")
+
+    def crt_to_f64(self, mag, neg, out, count, out_stride=1, stream=None):
+        check(lib.mfhe_crt_to_f64(self._h, _ptr(mag), _ptr(neg), count, _ptr(out), out_stride, _stream_ptr(stream)),
+              "crt_to_f64")
+        return out
+
+    def crt_compose_f64(self, src, out, npoly, ncoeff, out_stride=1, stream=None):
+        check(lib.mfhe_crt_compose_f64(self._h, _ptr(src), npoly, ncoeff, _ptr(out), out_stride, _stream_ptr(stream)),
+              "crt_compose_f64")
+        return out
+
+
+def fnwt_1d(data, tw, tw_shoup, dmod, dim, coeff_modulus_size, start_modulus_idx=0, batch=1, stream=None):
+    """phantom fnwt_1d (ntt/ntt_1d.cu) over raw table pointers; batch polys at once."""
+    check(lib.mfhe_fnwt_1d(_ptr(data), tw, tw_shoup, dmod, dim, coeff_modulus_size, start_modulus_idx, batch,
+                           _stream_ptr(stream)), "fnwt_1d")
+
+
+def inwt_1d(data, itw, itw_shoup, dmod, scalar, scalar_shoup, dim, coeff_modulus_size, start_modulus_idx=0, batch=1,
+            stream=None):
+    check(lib.mfhe_inwt_1d(_ptr(data), itw, itw_shoup, dmod, scalar, scalar_shoup, dim, coeff_modulus_size,
+                           start_modulus_idx, batch, _stream_ptr(stream)), "inwt_1d")
+
+
+# ---- host/device array helpers (uint64 stored in int64 tensors) ----
+def to_device_u64(arr, device="cuda"):
+    import numpy as np
+    import torch
+    a = np.ascontiguousarray(arr, dtype=np.uint64)
+    return torch.from_numpy(a.view(np.int64)).to(device)
+
+
+def to_host_u64(t):
+    import numpy as np
+    return t.detach().cpu().numpy().view(np.uint64)

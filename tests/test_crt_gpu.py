@@ -1,0 +1,105 @@
+"""GPU parity: RNS decompose and wide CRT compose / centre-lift / f64 vs the CPU oracle, bit-exact.
+
+Reference: quantize_coeff_to_rns_kernel (batched_encoder.cu:125-152),
+crt_compose_centerlift_big_kernel (encoder.cu:191-230), compose_big_pair_to_complex_by_delta
+(HE.cu:1007-1027), dequantize_exact_kernel (encoder.cu:112-150).
+"""
+import numpy as np
+import pytest
+
+pytestmark = pytest.mark.gpu
+
+RNS = [17592186435073, 17182765057, 17184541441, 17186120449, 17186515201, 17186909953,
+       17188883713, 17190462721, 17190857473, 17191844353, 17192831233]
+
+
+def _param_sets(orc):
+    return [
+        ("reference", RNS, 6),
+        ("C1-like L=1", orc.gen_primes(50, 1 << 14, 1), 12),
+        ("C3 L=8 50-bit", orc.gen_primes(50, 1 << 18, 8), 16),
+        ("C4 L=16", orc.gen_primes(50, 1 << 18, 16), 16),
+        ("C5 L=32", orc.gen_primes(50, 1 << 19, 32), 17),
+        ("60-bit L=5", orc.gen_primes(61, 1 << 10, 5), 8),
+    ]
+
+
+def _values(rng, count, delta):
+    z = rng.uniform(-1.0, 1.0, count)
+    z[:8] = [0.0, 0.5 / delta, -0.5 / delta, 1.5 / delta, -2.5 / delta, 1.0, -1.0, 2.0 ** 27 / delta]
+    return z
+
+
+def test_rns_decompose_matches_oracle(mfhe, orc):
+    import torch
+    rng = np.random.default_rng(0)
+    for name, moduli, log_n in _param_sets(orc):
+        for delta in (2.0 ** 35, 2.0 ** 40 + 3.0):
+            ctx = mfhe.Context(moduli, log_n, mfhe.CONV_PHANTOM, delta=delta)
+            npoly, nc = 3, 4096
+            z = _values(rng, npoly * nc, delta) * 1000.0
+            zt = torch.from_numpy(z).cuda()
+            out = torch.zeros(npoly * len(moduli) * nc, dtype=torch.int64, device="cuda")
+            ctx.rns_decompose(zt, out, npoly, nc)
+            torch.cuda.synchronize()
+            np.testing.assert_array_equal(mfhe.to_host_u64(out), orc.rns_decompose(z, npoly, nc, moduli, delta),
+                                          err_msg=name)
+            # strided (complex interleaved) input, as the encoder uses for re / im
+            zc = torch.from_numpy(np.stack([z, -z], 1).ravel().copy()).cuda()
+            ctx.rns_decompose(zc[1:], out, npoly, nc, in_stride=2)
+            torch.cuda.synchronize()
+            np.testing.assert_array_equal(mfhe.to_host_u64(out), orc.rns_decompose(-z, npoly, nc, moduli, delta))
+
+
+def test_crt_compose_and_f64_match_oracle(mfhe, orc):
+    import torch
+    rng = np.random.default_rng(1)
+    for name, moduli, log_n in _param_sets(orc):
+        ctx = mfhe.Context(moduli, log_n)
+        W = ctx.crt_words
+        assert W == orc.crt_words(moduli)
+        npoly, nc = 2, 3000
+        q = np.array(moduli, np.uint64)[None, :, None]
+        data = (rng.integers(0, 2 ** 63, (npoly, len(moduli), nc), dtype=np.uint64) % q)
+        # small centred values too (the decode regime): v in [-2^40, 2^40]
+        small = rng.integers(-(1 << 40), 1 << 40, nc)
+        data[1] = np.array([[int(v) % int(m) for v in small] for m in moduli], np.uint64)
+        data[1, :, :3] = np.array([[0, 1, int(m) - 1] for m in moduli], np.uint64)
+        data = data.ravel()
+        d = mfhe.to_device_u64(data)
+        mag = torch.zeros(npoly * nc * W, dtype=torch.int64, device="cuda")
+        neg = torch.zeros(npoly * nc, dtype=torch.uint8, device="cuda")
+        ctx.crt_compose(d, mag, neg, npoly, nc)
+        torch.cuda.synchronize()
+        omag, oneg = orc.crt_compose(data, npoly, len(moduli), nc, moduli, W)
+        np.testing.assert_array_equal(mfhe.to_host_u64(mag).reshape(-1, W), omag, err_msg=name)
+        np.testing.assert_array_equal(neg.cpu().numpy(), oneg, err_msg=name)
+        ref = orc.big_to_f64(omag, oneg, W, ctx.delta)
+        f = torch.zeros(npoly * nc, dtype=torch.float64, device="cuda")
+        ctx.crt_to_f64(mag, neg, f, npoly * nc)
+        torch.cuda.synchronize()
+        np.testing.assert_array_equal(f.cpu().numpy(), ref, err_msg=name)
+        f2 = torch.zeros(2 * npoly * nc, dtype=torch.float64, device="cuda")
+        ctx.crt_compose_f64(d, f2, npoly, nc, out_stride=2)
+        torch.cuda.synchronize()
+        np.testing.assert_array_equal(f2.cpu().numpy()[::2], ref, err_msg=name)
+
+
+def test_decompose_compose_roundtrip_full_size(mfhe):
+    """Size-independent property at C3 scale: compose_f64(decompose(z)) == round(z*delta)/delta."""
+    import torch
+    import oracle
+    moduli = oracle.gen_primes(50, 1 << 18, 8)
+    ctx = mfhe.Context(moduli, 16)
+    npoly, nc = 64, 1 << 16
+    g = torch.Generator(device="cuda").manual_seed(3)
+    z = torch.rand(npoly * nc, dtype=torch.float64, device="cuda", generator=g) * 2 - 1
+    r = torch.empty(npoly * 8 * nc, dtype=torch.int64, device="cuda")
+    ctx.rns_decompose(z, r, npoly, nc)
+    out = torch.empty_like(z)
+    ctx.crt_compose_f64(r, out, npoly, nc)
+    torch.cuda.synchronize()
+    zd = z * ctx.delta                     # exact (delta = 2^35)
+    expect = torch.trunc(zd + torch.copysign(torch.full_like(zd, 0.5), zd)) / ctx.delta   # llround: ties away
+    assert (torch.round(zd) != torch.trunc(zd + torch.copysign(torch.full_like(zd, 0.5), zd))).any()
+    assert torch.equal(out, expect)

@@ -1,0 +1,220 @@
+"""GPU parity: batched NTT kernels (through include/mfhe.h) vs the CPU oracle, bit-exact.
+
+Reference behaviour being matched: xy_ntt_forward/backward_phantom -> phantom fnwt_1d/inwt_1d
+(ntt_core.cu:443-460), xy_ntt_forward/backward_gl and custom_ntt_forward/backward
+(ntt_core.cu:394-431, 462-481), apply_gl_perm (ntt_core.cu:433-441).
+"""
+import numpy as np
+import pytest
+
+pytestmark = pytest.mark.gpu
+
+RNS = [17592186435073, 17182765057, 17184541441, 17186120449, 17186515201, 17186909953,
+       17188883713, 17190462721, 17190857473, 17191844353, 17192831233]
+
+
+def rand_residues(rng, batch, moduli, N):
+    q = np.array(moduli, dtype=np.uint64)[None, :, None]
+    return (rng.integers(0, 2 ** 63, (batch, len(moduli), N), dtype=np.uint64) % q).ravel()
+
+
+def _roundtrip(mfhe, orc, ctx, data, nl_moduli, log_n, arith):
+    import torch
+    ctx.set_arith(arith)
+    L_ = len(nl_moduli)
+    d = mfhe.to_device_u64(data)
+    ctx.ntt_fwd(d)
+    torch.cuda.synchronize()
+    got = mfhe.to_host_u64(d)
+    ref = orc.phantom_fwd(data, L_, log_n, nl_moduli)
+    np.testing.assert_array_equal(got, ref)
+    ctx.ntt_inv(d)
+    torch.cuda.synchronize()
+    np.testing.assert_array_equal(mfhe.to_host_u64(d), data)
+
+
+@pytest.mark.parametrize("log_n", list(range(1, 18)))
+@pytest.mark.parametrize("arith", [1, 2])
+def test_phantom_ntt_matches_oracle(mfhe, orc, log_n, arith):
+    N = 1 << log_n
+    moduli = orc.gen_primes(50 if arith == 1 else 61, 4 * N, 3)
+    if arith == 1:
+        moduli = orc.gen_primes(50, 4 * N, 3)
+    batch = max(1, min(5, (1 << 18) // (N * 3)))
+    ctx = mfhe.Context(moduli, log_n, mfhe.CONV_PHANTOM)
+    if arith == 2 and moduli[0] >= 2 ** 50:
+        assert ctx.info().arith == mfhe.ARITH_U64
+    rng = np.random.default_rng(log_n)
+    data = rand_residues(rng, batch, moduli, N)
+    _roundtrip(mfhe, orc, ctx, data, moduli, log_n, arith)
+
+
+@pytest.mark.parametrize("arith", [1, 2])
+def test_phantom_inverse_of_random_matches_oracle(mfhe, orc, arith):
+    import torch
+    log_n = 16
+    moduli = orc.gen_primes(49, 1 << 18, 2)
+    ctx = mfhe.Context(moduli, log_n)
+    ctx.set_arith(arith)
+    data = rand_residues(np.random.default_rng(1), 2, moduli, 1 << log_n)
+    d = mfhe.to_device_u64(data)
+    ctx.ntt_inv(d)
+    torch.cuda.synchronize()
+    np.testing.assert_array_equal(mfhe.to_host_u64(d), orc.phantom_inv(data, 2, log_n, moduli))
+
+
+@pytest.mark.parametrize("arith", [1, 2])
+def test_kat1_reference_geometry_roundtrip(mfhe, orc, arith):
+    """test_custom_ntt_roundtrip.cu:63-112 at reference geometry: n = 64, L = 11, batch 1 and 32768,
+    input (b+l+x+1) mod q; forward must also equal the oracle (phantom) bit-exactly."""
+    ctx = mfhe.Context(RNS, 6)
+    for batch in (1, 512 * 64):
+        b = np.arange(batch, dtype=np.uint64)[:, None, None]
+        l = np.arange(11, dtype=np.uint64)[None, :, None]
+        x = np.arange(64, dtype=np.uint64)[None, None, :]
+        data = ((b + l + x + 1) % np.array(RNS, np.uint64)[None, :, None]).ravel()
+        _roundtrip(mfhe, orc, ctx, data, RNS, 6, arith)
+
+
+def test_extreme_moduli_and_values(mfhe, orc):
+    """F64 path edge: the largest primes below 2^50 with all-(q-1) and all-zero inputs."""
+    import torch
+    for log_n in (6, 12, 16, 17):
+        N = 1 << log_n
+        moduli = orc.gen_primes(50, 2 * N, 2)
+        assert all(q < 2 ** 50 for q in moduli)
+        ctx = mfhe.Context(moduli, log_n)
+        assert ctx.info().arith == mfhe.ARITH_F64
+        for fill in ("max", "zero", "alt"):
+            q = np.array(moduli, np.uint64)[None, :, None]
+            if fill == "max":
+                data = np.broadcast_to(q - 1, (2, 2, N)).copy().ravel()
+            elif fill == "zero":
+                data = np.zeros(2 * 2 * N, np.uint64)
+            else:
+                data = np.where(np.arange(N)[None, None, :] % 2 == 0, q - 1, 0).astype(np.uint64)
+                data = np.broadcast_to(data, (2, 2, N)).copy().ravel()
+            d = mfhe.to_device_u64(data)
+            ctx.ntt_fwd(d)
+            torch.cuda.synchronize()
+            np.testing.assert_array_equal(mfhe.to_host_u64(d), orc.phantom_fwd(data, 2, log_n, moduli))
+            ctx.ntt_inv(d)
+            torch.cuda.synchronize()
+            np.testing.assert_array_equal(mfhe.to_host_u64(d), data)
+
+
+def test_limb_subrange(mfhe, orc):
+    """start_limb / nlimbs select moduli start..start+nl-1 (the fnwt_1d start_modulus_idx)."""
+    import torch
+    log_n = 12
+    moduli = orc.gen_primes(50, 1 << 14, 5)
+    ctx = mfhe.Context(moduli, log_n)
+    sub = moduli[2:4]
+    data = rand_residues(np.random.default_rng(2), 3, sub, 1 << log_n)
+    d = mfhe.to_device_u64(data)
+    ctx.ntt_fwd(d, batch=3, start_limb=2, nlimbs=2)
+    torch.cuda.synchronize()
+    np.testing.assert_array_equal(mfhe.to_host_u64(d), orc.phantom_fwd(data, 2, log_n, sub))
+
+
+@pytest.mark.parametrize("log_n", [2, 6, 9, 12, 14])
+@pytest.mark.parametrize("arith", [1, 2])
+def test_gl_and_cyclic_match_oracle(mfhe, orc, log_n, arith):
+    import torch
+    N = 1 << log_n
+    moduli = RNS if log_n <= 6 else orc.gen_primes(48, 4 * N, 3)
+    ctx = mfhe.Context(moduli, log_n, mfhe.CONV_PHANTOM | mfhe.CONV_GL)
+    ctx.set_arith(arith)
+    data = rand_residues(np.random.default_rng(log_n), 3, moduli, N)
+    for fwd, inv, ofwd, oinv in ((ctx.gl_ntt_fwd, ctx.gl_ntt_inv, orc.gl_fwd, orc.gl_bwd),
+                                 (ctx.cyclic_ntt_fwd, ctx.cyclic_ntt_inv, orc.custom_fwd, orc.custom_bwd)):
+        d = mfhe.to_device_u64(data)
+        fwd(d)
+        torch.cuda.synchronize()
+        ref = ofwd(data, len(moduli), N, moduli)
+        np.testing.assert_array_equal(mfhe.to_host_u64(d), ref)
+        d2 = mfhe.to_device_u64(ref)
+        inv(d2)
+        torch.cuda.synchronize()
+        np.testing.assert_array_equal(mfhe.to_host_u64(d2), oinv(ref, len(moduli), N, moduli))
+        np.testing.assert_array_equal(mfhe.to_host_u64(d2), data)
+
+
+def test_kat4_gl_product_on_gpu(mfhe, orc):
+    """test_custom_ntt_roundtrip.cu:256-319 on the device: product mod X^n - i."""
+    import torch
+    q = RNS[0]
+    n = 64
+    ctx = mfhe.Context([q], 6, mfhe.CONV_GL)
+    psi4n = orc.L.orc_get_psi4n(q, n)
+    iroot = pow(psi4n, n, q)
+    a = np.array([(j + 1) % q for j in range(n)], np.uint64)
+    b = np.array([(j + 3) % q for j in range(n)], np.uint64)
+    da, db = mfhe.to_device_u64(a), mfhe.to_device_u64(b)
+    ctx.gl_ntt_fwd(da)
+    ctx.gl_ntt_fwd(db)
+    torch.cuda.synchronize()
+    fa, fb = mfhe.to_host_u64(da), mfhe.to_host_u64(db)
+    prod = np.array([int(x) * int(y) % q for x, y in zip(fa, fb)], np.uint64)
+    dp = mfhe.to_device_u64(prod)
+    ctx.gl_ntt_inv(dp)
+    torch.cuda.synchronize()
+    ref = [0] * n
+    for j in range(n):
+        for k in range(n):
+            p = int(a[j]) * int(b[k]) % q
+            if j + k < n:
+                ref[j + k] = (ref[j + k] + p) % q
+            else:
+                ref[j + k - n] = (ref[j + k - n] + p * iroot) % q
+    assert [int(v) for v in mfhe.to_host_u64(dp)] == ref
+
+
+def test_gl_perm_matches_oracle(mfhe, orc):
+    import torch
+    ctx = mfhe.Context(RNS, 6, mfhe.CONV_GL)
+    data = rand_residues(np.random.default_rng(9), 7, RNS, 64)
+    d = mfhe.to_device_u64(data)
+    for inverse in (False, True):
+        out = torch.empty_like(d)
+        ctx.gl_perm(d, out, 7, inverse=inverse)
+        torch.cuda.synchronize()
+        np.testing.assert_array_equal(mfhe.to_host_u64(out), orc.gl_perm(data, 11, 64, inverse))
+
+
+def test_raw_phantom_surface(mfhe, orc):
+    """fnwt_1d / inwt_1d over the context's phantom-format tables (DNTTTable surface)."""
+    import torch
+    ctx = mfhe.Context(RNS, 6)
+    tw, tws, itw, itws, ninv, ninvs, dmod = ctx.ntt_tables()
+    data = rand_residues(np.random.default_rng(4), 1, RNS, 64)
+    d = mfhe.to_device_u64(data)
+    mfhe.fnwt_1d(d, tw, tws, dmod, 64, 11, 0)
+    torch.cuda.synchronize()
+    np.testing.assert_array_equal(mfhe.to_host_u64(d), orc.phantom_fwd(data, 11, 6, RNS))
+    mfhe.inwt_1d(d, itw, itws, dmod, ninv, ninvs, 64, 11, 0)
+    torch.cuda.synchronize()
+    np.testing.assert_array_equal(mfhe.to_host_u64(d), data)
+    # tables equal the oracle's phantom host tables
+    t = np.zeros(11 * 64, np.uint64)
+    import ctypes
+    import hip_util
+    hip_util.d2h(t, tw)
+    for l in (0, 10):
+        otw = orc.phantom_tables(6, RNS[l])[0]
+        np.testing.assert_array_equal(t[l * 64:(l + 1) * 64], otw)
+
+
+def test_invalid_arguments(mfhe):
+    ctx = mfhe.Context(RNS, 6)
+    import torch
+    d = torch.zeros(64 * 11, dtype=torch.int64, device="cuda")
+    with pytest.raises(mfhe.MfheError) as e:
+        ctx.ntt_fwd(d, batch=1, start_limb=5, nlimbs=7)
+    assert e.value.code == mfhe.EINVAL
+    with pytest.raises(mfhe.MfheError) as e:
+        ctx.gl_ntt_fwd(d)
+    assert e.value.code == mfhe.ENOTREADY
+    with pytest.raises(mfhe.MfheError) as e:
+        mfhe.Context([97], 6)   # 2N = 128 does not divide 96
+    assert e.value.code == mfhe.EUNSUPPORTED
