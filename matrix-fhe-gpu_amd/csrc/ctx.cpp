@@ -314,6 +314,30 @@ extern "C" int mfhe_ctx_set_arith(mfhe_ctx* c, int arith) {
     return MFHE_OK;
 }
 
+extern "C" int mfhe_ctx_set_option(mfhe_ctx* c, int opt, int64_t v) {
+    if (!c) return set_error(MFHE_EINVAL, "mfhe_ctx_set_option: null ctx");
+    switch (opt) {
+        case MFHE_OPT_NTT_CHUNK_BYTES:
+            if (v < 0) return set_error(MFHE_EINVAL, "chunk bytes must be >= 0");
+            c->ntt_chunk_bytes = v;
+            return MFHE_OK;
+        case MFHE_OPT_NTT_PLAN:
+            if (v < 0 || v > 2) return set_error(MFHE_EINVAL, "plan must be 0, 1 or 2");
+            c->ntt_plan = (int)v;
+            return MFHE_OK;
+        default: return set_error(MFHE_EINVAL, "unknown option");
+    }
+}
+
+extern "C" int mfhe_ctx_get_option(const mfhe_ctx* c, int opt, int64_t* v) {
+    if (!c || !v) return set_error(MFHE_EINVAL, "mfhe_ctx_get_option: null argument");
+    switch (opt) {
+        case MFHE_OPT_NTT_CHUNK_BYTES: *v = c->ntt_chunk_bytes; return MFHE_OK;
+        case MFHE_OPT_NTT_PLAN: *v = c->ntt_plan; return MFHE_OK;
+        default: return set_error(MFHE_EINVAL, "unknown option");
+    }
+}
+
 extern "C" int mfhe_ctx_get_moduli(const mfhe_ctx* c, uint64_t* out, int count) {
     if (!c || !out || count < c->L) return set_error(MFHE_EINVAL, "mfhe_ctx_get_moduli: bad argument");
     std::memcpy(out, c->moduli.data(), (size_t)c->L * 8);

@@ -58,6 +58,8 @@ struct mfhe_ctx {
     double delta = 0.0;
     int device = 0;
     std::vector<uint64_t> moduli;
+    int64_t ntt_chunk_bytes = 192ll << 20;  // measured best at N = 2^15..2^17 (profiles/r01_ntt_sweep.txt)
+    int ntt_plan = 0;
 
     mfhe::LimbConst* d_limbs = nullptr;  // [L]
     uint64_t* d_dmod = nullptr;          // [L][3] phantom DModulus {value, const_ratio[2]}

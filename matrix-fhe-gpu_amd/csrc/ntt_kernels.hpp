@@ -102,29 +102,33 @@ __global__ __launch_bounds__(NG * (1 << (LOG_G - LOG_R))) void ntt_pass_kernel(P
     const int logN = a.logN;
     const int logS = logN - a.s0 - LOG_G;
     const uint64_t S = 1ull << logS;
-    const uint64_t gpp = S << a.s0;  // groups per polynomial-limb
-    const uint64_t npl = a.batch * (uint64_t)a.nl;
+    const int log_gpp = logS + a.s0;  // log2(groups per polynomial-limb)
+    const uint32_t npl = (uint32_t)(a.batch * (uint64_t)a.nl);   // launcher guarantees < 2^32
     const uint32_t lb = xcd_remap(blockIdx.x, a.nblocks);
 
-    uint64_t v, hi, lo;
+    uint32_t v;
+    uint64_t hi, lo;
     if constexpr (COLS) {
-        const uint64_t tpp = gpp / NG, cols_tiles = S / NG;
-        v = lb / tpp;
-        const uint64_t tile = lb % tpp;
-        hi = tile / cols_tiles;
-        lo = (tile % cols_tiles) * NG + gl;
+        // tiles of NG consecutive columns; tiles per poly = 2^log_gpp / NG
+        constexpr int LOG_NG = __builtin_ctz(NG);
+        const int log_tpp = log_gpp - LOG_NG, log_ct = logS - LOG_NG;
+        v = lb >> log_tpp;
+        const uint32_t tile = lb & ((1u << log_tpp) - 1);
+        hi = tile >> log_ct;
+        lo = ((uint64_t)(tile & ((1u << log_ct) - 1)) << LOG_NG) + gl;
     } else {
         const uint64_t gid = (uint64_t)lb * NG + gl;
-        v = gid / gpp;
-        const uint64_t rem = gid % gpp;
+        v = (uint32_t)(gid >> log_gpp);
+        const uint64_t rem = gid & ((1ull << log_gpp) - 1);
         hi = rem >> logS;
         lo = rem & (S - 1);
     }
     const bool active = v < npl;
     if (!active) v = 0;
     // virtual poly index is limb-major: v = l * batch + b
-    const int l = (int)(v / a.batch);
-    const uint64_t b = v % a.batch;
+    const uint32_t bt = (uint32_t)a.batch;
+    const int l = (int)(v / bt);
+    const uint64_t b = v - (uint32_t)l * bt;
     const int mod = a.start_limb + l;
     const uint64_t N = 1ull << logN;
     uint64_t* base = a.data + (b * (uint64_t)a.nl + (uint64_t)l) * N;
@@ -164,7 +168,9 @@ __global__ __launch_bounds__(NG * (1 << (LOG_G - LOG_R))) void ntt_pass_kernel(P
 #pragma unroll
     for (int k = 0; k < R; ++k) {
         const uint32_t g = Gm::g_of(r_load, tau, k);
-        const uint64_t raw = active ? base[jidx(g)] : 0;
+        // unconditional: inactive tail threads point at a valid polynomial (v = 0); a per-element
+        // "active ? load : 0" makes hipcc branch around every load with a vmcnt(0) each.
+        const uint64_t raw = base[jidx(g)];
         x[k] = IN_RAW ? A::from_raw(raw) : A::from_u64(raw);
         if constexpr (TWIST && !INV) x[k] = ar.mulmod(x[k], a.twist.get(twoff + jidx(g)));
     }

@@ -22,6 +22,7 @@ HEADER = REPO_ROOT / "include" / "mfhe.h"
 OK, EINVAL, EUNSUPPORTED, EHIP, ENOMEM, ENOTREADY = 0, 1, 2, 3, 4, 5
 CONV_PHANTOM, CONV_GL, CONV_WCRT = 1, 2, 4
 ARITH_AUTO, ARITH_F64, ARITH_U64 = 0, 1, 2
+OPT_NTT_CHUNK_BYTES, OPT_NTT_PLAN = 1, 2
 
 #: reference parameters (include/core/config.h:7-52)
 RNS_MODULI = [
@@ -74,6 +75,8 @@ _sig("mfhe_ctx_destroy", [_vp])
 _sig("mfhe_ctx_get_info", [_vp, ctypes.POINTER(CtxInfo)])
 _sig("mfhe_ctx_set_arith", [_vp, ctypes.c_int])
 _sig("mfhe_ctx_get_moduli", [_vp, _u64p, ctypes.c_int])
+_sig("mfhe_ctx_set_option", [_vp, ctypes.c_int, ctypes.c_int64])
+_sig("mfhe_ctx_get_option", [_vp, ctypes.c_int, ctypes.POINTER(ctypes.c_int64)])
 for _n in ("mfhe_ntt_fwd", "mfhe_ntt_inv", "mfhe_gl_ntt_fwd", "mfhe_gl_ntt_inv", "mfhe_cyclic_ntt_fwd",
            "mfhe_cyclic_ntt_inv"):
     _sig(_n, [_vp, _vp, _sz, ctypes.c_int, ctypes.c_int, _vp])
@@ -151,6 +154,14 @@ class Context:
 
     def set_arith(self, arith: int) -> None:
         check(lib.mfhe_ctx_set_arith(self._h, arith), "set_arith")
+
+    def set_option(self, opt: int, value: int) -> None:
+        check(lib.mfhe_ctx_set_option(self._h, opt, int(value)), "set_option")
+
+    def get_option(self, opt: int) -> int:
+        v = ctypes.c_int64()
+        check(lib.mfhe_ctx_get_option(self._h, opt, ctypes.byref(v)), "get_option")
+        return v.value
 
     def close(self):
         if getattr(self, "_h", None):

@@ -218,3 +218,25 @@ def test_invalid_arguments(mfhe):
     with pytest.raises(mfhe.MfheError) as e:
         mfhe.Context([97], 6)   # 2N = 128 does not divide 96
     assert e.value.code == mfhe.EUNSUPPORTED
+
+
+@pytest.mark.parametrize("log_n", [12, 13, 14, 15, 16, 17])
+def test_two_pass_plans_and_chunking(mfhe, orc, log_n):
+    """MFHE_OPT_NTT_PLAN = 2 (two passes from log_n 12) and batch chunking (uneven tail chunk)."""
+    import torch
+    N = 1 << log_n
+    moduli = orc.gen_primes(50, 4 * N, 3)
+    ctx = mfhe.Context(moduli, log_n)
+    ctx.set_option(mfhe.OPT_NTT_PLAN, 2)
+    batch = 5
+    ctx.set_option(mfhe.OPT_NTT_CHUNK_BYTES, 2 * 3 * N * 8)   # chunks of 2 polys -> 2, 2, 1
+    data = rand_residues(np.random.default_rng(100 + log_n), batch, moduli, N)
+    for arith in (1, 2):
+        ctx.set_arith(arith)
+        d = mfhe.to_device_u64(data)
+        ctx.ntt_fwd(d)
+        torch.cuda.synchronize()
+        np.testing.assert_array_equal(mfhe.to_host_u64(d), orc.phantom_fwd(data, 3, log_n, moduli))
+        ctx.ntt_inv(d)
+        torch.cuda.synchronize()
+        np.testing.assert_array_equal(mfhe.to_host_u64(d), data)

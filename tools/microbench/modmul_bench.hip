@@ -60,6 +60,53 @@ __global__ void k_fp64(double* out, double q, double w, double wq) {
     out[tid] = acc;
 }
 
+// FP64 butterfly with magic-constant rounding instead of v_rndne_f64
+__global__ void k_fp64_magic(double* out, double q, double w, double wq) {
+    double v[VPT], u[VPT];
+    uint64_t tid = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x;
+    for (int i = 0; i < VPT; ++i) { v[i] = (double)((tid * 7919u + i * 104729u) % (uint64_t)q); u[i] = (double)((tid + i) % (uint64_t)q); }
+    const double M = 6755399441055744.0;  // 1.5 * 2^52
+    for (int it = 0; it < ITERS; ++it) {
+#pragma unroll
+        for (int i = 0; i < VPT; ++i) {
+            double hi = v[i] * w;
+            double lo = fma(v[i], w, -hi);
+            double k = fma(v[i], wq, M) - M;
+            double t = fma(-k, q, hi) + lo;
+            double x = u[i] + t;
+            double y = u[i] - t;
+            x = (x > 0.5 * q) ? x - q : x;
+            y = (y < -0.5 * q) ? y + q : y;
+            u[i] = x; v[i] = y;
+        }
+    }
+    double acc = 0;
+    for (int i = 0; i < VPT; ++i) acc += u[i] + v[i];
+    out[tid] = acc;
+}
+
+// plain FP64 CT butterfly without range folding (what the NTT kernel does between reductions)
+__global__ void k_fp64_plain(double* out, double q, double w, double wq) {
+    double v[VPT], u[VPT];
+    uint64_t tid = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x;
+    for (int i = 0; i < VPT; ++i) { v[i] = (double)((tid * 7919u + i * 104729u) % (uint64_t)q); u[i] = (double)((tid + i) % (uint64_t)q); }
+    for (int it = 0; it < ITERS; ++it) {
+#pragma unroll
+        for (int i = 0; i < VPT; ++i) {
+            double hi = v[i] * w;
+            double lo = fma(v[i], w, -hi);
+            double k = rint(v[i] * wq);
+            double t = fma(-k, q, hi) + lo;
+            double x = u[i] + t;
+            double y = u[i] - t;
+            u[i] = y * 0.5; v[i] = x * 0.5;   // keep bounded, 1 op each
+        }
+    }
+    double acc = 0;
+    for (int i = 0; i < VPT; ++i) acc += u[i] + v[i];
+    out[tid] = acc;
+}
+
 // 64-bit Montgomery butterfly (R = 2^64), lazy.
 __global__ void k_int_mont(uint64_t* out, uint64_t q, uint64_t wm, uint64_t qinv_neg) {
     uint64_t v[VPT], u[VPT];
@@ -119,6 +166,16 @@ int main() {
         CHECK(hipEventRecord(b)); CHECK(hipEventSynchronize(b));
         CHECK(hipEventElapsedTime(&ms, a, b));
         printf("fp64       butterflies/s = %.3e  (%.3f ms)\n", bfl / (ms * 1e-3), ms);
+        CHECK(hipEventRecord(a));
+        k_fp64_magic<<<blocks, threads>>>((double*)d_out, (double)q, (double)w, (double)w / (double)q);
+        CHECK(hipEventRecord(b)); CHECK(hipEventSynchronize(b));
+        CHECK(hipEventElapsedTime(&ms, a, b));
+        printf("fp64_magic butterflies/s = %.3e  (%.3f ms)\n", bfl / (ms * 1e-3), ms);
+        CHECK(hipEventRecord(a));
+        k_fp64_plain<<<blocks, threads>>>((double*)d_out, (double)q, (double)w, (double)w / (double)q);
+        CHECK(hipEventRecord(b)); CHECK(hipEventSynchronize(b));
+        CHECK(hipEventElapsedTime(&ms, a, b));
+        printf("fp64_plain butterflies/s = %.3e  (%.3f ms)\n", bfl / (ms * 1e-3), ms);
         CHECK(hipEventRecord(a));
         k_int_mont<<<blocks, threads>>>(d_out, q | 1, w, 0x9E3779B97F4A7C15ULL);
         CHECK(hipEventRecord(b)); CHECK(hipEventSynchronize(b));
