@@ -10,6 +10,8 @@
 
 #include <algorithm>
 #include <cmath>
+#include <complex>
+#include <thread>
 #include <cstring>
 #include <string>
 #include <vector>
@@ -133,6 +135,7 @@ static int build_crt(mfhe_ctx* c) {
     Q.resize(W);
     std::vector<uint64_t> Qh(W), M((size_t)L * W), inv((size_t)L * 2), mu((size_t)L * 2);
     std::vector<double> qinv(L);
+    std::vector<uint64_t> r64(L);
     uint64_t carry = 0;
     for (int i = W - 1; i >= 0; --i) {
         Qh[i] = (Q[i] >> 1) | (carry << 63);
@@ -154,11 +157,98 @@ static int build_crt(mfhe_ctx* c) {
         qinv[k] = 1.0 / (double)q;
         mu[2 * k] = q;
         mu[2 * k + 1] = (uint64_t)((((hm::u128)1) << 64) / q);
+        r64[k] = (uint64_t)((((hm::u128)1) << 64) % q);
     }
     int rc;
     if ((rc = upload(c, &c->d_crt_M, M)) || (rc = upload(c, &c->d_crt_inv, inv)) ||
         (rc = upload(c, &c->d_crt_qinv, qinv)) || (rc = upload(c, &c->d_crt_Q, Q)) ||
-        (rc = upload(c, &c->d_crt_Qhalf, Qh)) || (rc = upload(c, &c->d_rns_mu, mu)))
+        (rc = upload(c, &c->d_crt_Qhalf, Qh)) || (rc = upload(c, &c->d_rns_mu, mu)) ||
+        (rc = upload(c, &c->d_r64, r64)))
+        return rc;
+    return MFHE_OK;
+}
+
+// W-axis tables: init_wntt_tables (HE.cu:237-273), init_wdft_tables (HE.cu:275-310),
+// Encoder::init_complex_matrices (encoder.cu:425-444).
+static int build_wcrt(mfhe_ctx* c) {
+    const int PHI = mfhe_ctx::PHI, L = c->L;
+    uint16_t exp[512];
+    hm::wcrt_exponents(exp);
+    std::vector<uint64_t> V((size_t)L * PHI * PHI), Vi((size_t)L * PHI * PHI);
+    std::vector<int> bad(L, 0);
+    std::vector<std::thread> th;
+    for (int l = 0; l < L; ++l)
+        th.emplace_back([&, l] {
+            const uint64_t q = c->moduli[l];
+            const uint64_t eta = hm::find_eta771(q);
+            if (!eta) { bad[l] = 1; return; }
+            std::vector<uint64_t> xs(PHI), inv;
+            for (int w = 0; w < PHI; ++w) {
+                const uint64_t root = hm::powmod(eta, exp[w], q);
+                xs[w] = root;
+                uint64_t cur = 1;
+                for (int r = 0; r < PHI; ++r) {
+                    V[((size_t)l * PHI + w) * PHI + r] = cur;
+                    cur = hm::mulmod(cur, root, q);
+                }
+            }
+            if (!hm::vandermonde_inverse_mod(xs, q, inv)) { bad[l] = 1; return; }
+            std::copy(inv.begin(), inv.end(), Vi.begin() + (size_t)l * PHI * PHI);
+        });
+    for (auto& t : th) t.join();
+    for (int l = 0; l < L; ++l)
+        if (bad[l]) return set_error(MFHE_EUNSUPPORTED, "W-CRT table construction failed (no order-771 root)");
+    // complex W-DFT: V[w][r] = root_w^r by repeated multiplication, as HE.cu:282-290
+    std::vector<double> wd((size_t)PHI * PHI * 2), wdi;
+    {
+        const double p = 771.0, two_pi = 6.283185307179586476925286766559;
+        for (int w = 0; w < PHI; ++w) {
+            const double ang = two_pi * (double)exp[w] / p;
+            const std::complex<double> root(std::cos(ang), std::sin(ang));
+            std::complex<double> cur(1.0, 0.0);
+            for (int r = 0; r < PHI; ++r) {
+                wd[((size_t)w * PHI + r) * 2] = cur.real();
+                wd[((size_t)w * PHI + r) * 2 + 1] = cur.imag();
+                cur *= root;
+            }
+        }
+        std::vector<double> a = wd;
+        if (!hm::complex_inverse_gj(a, PHI, wdi)) return set_error(MFHE_EUNSUPPORTED, "W-DFT matrix singular");
+    }
+    // XY encoder matrices
+    const int n = (int)c->N;
+    std::vector<double2> eV((size_t)n * n), eVT((size_t)n * n), eVi((size_t)n * n), eViT((size_t)n * n);
+    {
+        const double PI = 3.141592653589793;
+        auto cmul = [](double2 a, double2 b) { return make_double2(a.x * b.x - a.y * b.y, a.x * b.y + a.y * b.x); };
+        for (int j = 0; j < n; ++j) {
+            uint64_t e = 1, b5 = 5;
+            int p = j;
+            while (p > 0) { if (p & 1) e = (e * b5) % (uint64_t)(4 * n); b5 = (b5 * b5) % (uint64_t)(4 * n); p >>= 1; }
+            const double ang = 2.0 * PI * (double)e / (4.0 * n);
+            const double2 z = make_double2(std::cos(ang), std::sin(ang)), zi = make_double2(z.x, -z.y);
+            const double2 sc = make_double2(1.0 / n, 0.0);
+            double2 cc = make_double2(1, 0), ci = make_double2(1, 0);
+            for (int k = 0; k < n; ++k) {
+                eV[(size_t)j * n + k] = cc;
+                eVi[(size_t)k * n + j] = cmul(ci, sc);
+                cc = cmul(cc, z);
+                ci = cmul(ci, zi);
+            }
+        }
+        for (int r = 0; r < n; ++r)
+            for (int cc2 = 0; cc2 < n; ++cc2) {
+                eVT[(size_t)cc2 * n + r] = eV[(size_t)r * n + cc2];
+                eViT[(size_t)cc2 * n + r] = eVi[(size_t)r * n + cc2];
+            }
+    }
+    std::vector<double2> wdv((size_t)PHI * PHI), wdvi((size_t)PHI * PHI);
+    std::memcpy(wdv.data(), wd.data(), wd.size() * 8);
+    std::memcpy(wdvi.data(), wdi.data(), wdi.size() * 8);
+    int rc;
+    if ((rc = upload(c, &c->d_wV, V)) || (rc = upload(c, &c->d_wVinv, Vi)) || (rc = upload(c, &c->d_wdV, wdv)) ||
+        (rc = upload(c, &c->d_wdVinv, wdvi)) || (rc = upload(c, &c->d_encV, eV)) || (rc = upload(c, &c->d_encVT, eVT)) ||
+        (rc = upload(c, &c->d_encVi, eVi)) || (rc = upload(c, &c->d_encViT, eViT)))
         return rc;
     return MFHE_OK;
 }
@@ -182,6 +272,8 @@ static int ctx_create_impl(const uint64_t* moduli, int L, int logN, int conv, do
             return set_error(MFHE_EUNSUPPORTED, "modulus " + std::to_string(q) + " has no primitive 4N-th root (GL)");
         if ((conv & MFHE_CONV_WCRT) && (q - 1) % 771 != 0)
             return set_error(MFHE_EUNSUPPORTED, "modulus " + std::to_string(q) + " has no 771-th root (W-CRT)");
+        if ((conv & MFHE_CONV_WCRT) && q >= (1ull << 59))
+            return set_error(MFHE_EUNSUPPORTED, "W-CRT needs moduli < 2^59 (512-term u128 accumulation)");
     }
     mfhe_ctx* c = new mfhe_ctx();
     c->L = L;
@@ -268,6 +360,7 @@ static int ctx_create_impl(const uint64_t* moduli, int L, int logN, int conv, do
         if ((rc = upload(c, &c->gl_perm, perm)) || (rc = upload(c, &c->gl_inv_perm, iperm))) return fail(rc);
     }
     if ((rc = build_crt(c))) return fail(rc);
+    if ((conv & MFHE_CONV_WCRT) && (rc = build_wcrt(c))) return fail(rc);
     *out = c;
     return MFHE_OK;
 }
@@ -287,6 +380,7 @@ extern "C" int mfhe_ctx_create(const uint64_t* moduli, int L, int log_n, int con
 
 extern "C" int mfhe_ctx_destroy(mfhe_ctx* c) {
     if (!c) return MFHE_OK;
+    if (c->ws) (void)hipFree(c->ws);
     for (void* p : c->allocs) (void)hipFree(p);
     delete c;
     return MFHE_OK;

@@ -1,0 +1,44 @@
+// gemm.hpp -- dense contractions on the W and XY axes.
+//
+//  * modular GEMM  C[m][p] = sum_k A[m][k] B[k][p] mod q   (W-CRT, HE.cu:716-781, 1245-1270)
+//    u64 operands (< 2^59), exact u128 accumulation over K = 512, one reduction per output.
+//    The reference does an __int128 % per term (HE.cu:742); we reduce once.
+//  * complex GEMM  C = A B  in FP64                           (W-DFT HE.cu:1147-1172, w_idft
+//    batched_encoder.cu:104-123, XY DFT mat_mul_kernel_complex encoder.cu:318-326)
+//
+// Both are LDS-tiled 64x64 output tiles, 256 threads, 4x4 outputs per thread.  B and C are
+// addressed through a (k|m, pos) -> offset map  k*sK + (pos >> log_n)*sY + (pos & (n-1)) so the
+// same kernel serves matrix-major and poly-major layouts (HE.cu:744-746, 773, 778).
+#pragma once
+#include <hip/hip_runtime.h>
+
+#include <cstdint>
+
+namespace mfhe {
+
+struct ModGemmArgs {
+    const uint64_t* A;     // [L][M][K] row-major, limb stride aL
+    const uint64_t* B;     // limb l at B + l*bL
+    uint64_t* C;           // limb l at C + l*cL
+    uint64_t aL, bL, cL;
+    uint64_t sbK, sbY, scM, scY;
+    int M, K, log_n;
+    uint32_t P;
+    const uint64_t* qmu;   // [L][2] (q, floor(2^64/q))
+    const uint64_t* r64;   // [L] 2^64 mod q
+};
+
+struct CGemmArgs {
+    const double2* A;      // batch b at A + b*aB, row-major [M][K] (lda = K)
+    const double2* B;      // batch b at B + b*bB, element (k,p) at k*sbK + (p>>log_n)*sbY + (p&(n-1))
+    double2* C;            // batch b at C + b*cB, element (m,p) at m*scM + (p>>log_n)*scY + (p&(n-1))
+    uint64_t aB, bB, cB;
+    uint64_t sbK, sbY, scM, scY;
+    int M, K, log_n;
+    uint32_t P;
+};
+
+int launch_mod_gemm(const ModGemmArgs& a, int L, hipStream_t s);
+int launch_cgemm(const CGemmArgs& a, int batch, hipStream_t s);
+
+}  // namespace mfhe

@@ -1,0 +1,547 @@
+// he.hip -- W-axis transforms, XY encoder transforms, layouts, samplers and the
+// encode / keygen / encrypt / decrypt / decode pipelines at reference geometry.
+//
+// Reference: src/core/HE.cu (W-CRT 437-470, 716-781, 1029-1114, 1245-1270; samplers 564-627,
+// 690-713; ring ops 509-560; layouts 1330-1368; pipelines 1272-1307, 1370-1708),
+// src/core/batched_encoder.cu:161-228, src/core/encoder.cu:425-501.
+//
+// Differences by design (results identical): one batched launch instead of per-lane launch loops
+// (batched_encoder.cu:192-196, HE.cu:1653-1668, 1676-1679); no per-call malloc/free (a context
+// workspace instead); the W-CRT output is written straight into the layout the caller needs;
+// CRT compose and f64/delta are fused.
+#include <hip/hip_runtime.h>
+
+#include <cmath>
+
+#include "gemm.hpp"
+#include "mfhe_ctx.hpp"
+
+extern "C" int mfhe_ntt_fwd(mfhe_ctx*, uint64_t*, size_t, int, int, mfhe_stream_t);
+extern "C" int mfhe_ntt_inv(mfhe_ctx*, uint64_t*, size_t, int, int, mfhe_stream_t);
+extern "C" int mfhe_crt_compose(mfhe_ctx*, const uint64_t*, size_t, size_t, uint64_t*, uint8_t*, mfhe_stream_t);
+extern "C" int mfhe_crt_compose_f64(mfhe_ctx*, const uint64_t*, size_t, size_t, double*, size_t, mfhe_stream_t);
+extern "C" int mfhe_rns_decompose(mfhe_ctx*, const double*, size_t, size_t, size_t, uint64_t*, mfhe_stream_t);
+
+namespace mfhe {
+
+static inline dim3 g1(uint64_t total, uint32_t th = 256) { return dim3((uint32_t)((total + th - 1) / th)); }
+
+// ---------------- layouts: HE.cu:1330-1368 ----------------
+template <bool TO_POLY>
+__global__ void layout_kernel(const uint64_t* __restrict__ in, uint64_t* __restrict__ out, int log_n, int L,
+                              uint64_t total) {
+    const uint64_t i = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x;   // matrix-major index
+    if (i >= total) return;
+    const uint64_t n = 1ull << log_n, n2 = n * n;
+    const uint64_t x = i & (n - 1), y = (i >> log_n) & (n - 1);
+    const uint64_t wl = i >> (2 * log_n), l = wl % L, w = wl / L;
+    const uint64_t p = ((w * n + y) * L + l) * n + x;
+    (void)n2;
+    if (TO_POLY) out[p] = in[i];
+    else out[i] = in[p];
+}
+
+// ---------------- samplers (deterministic in the element index) ----------------
+// ternary_secret_kernel HE.cu:690-713, [phi][L][n]
+__global__ void ternary_kernel(uint64_t* s, const uint64_t* qmu, int L, int log_n, uint64_t total) {
+    const uint64_t idx = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x;
+    if (idx >= total) return;
+    const uint64_t n = 1ull << log_n, single = (uint64_t)L * n;
+    const uint64_t off = idx % single;
+    const int limb = (int)(off >> log_n);
+    const uint64_t coeff = off & (n - 1), poly = idx / single;
+    const uint64_t t = poly * 1315423911ULL + coeff * 2654435761ULL;
+    const int r = (int)((t * 11400714819323198485ULL) % 3ULL);
+    const uint64_t q = qmu[2 * limb];
+    s[idx] = (r == 0) ? 0 : (r == 1) ? 1 : q - 1;
+}
+
+// uniform_random_kernel HE.cu:564-578, matrix-major [phi][L][n*n]
+__global__ void uniform_kernel(uint64_t* a, const uint64_t* qmu, int L, int log_n, uint64_t total) {
+    const uint64_t idx = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x;
+    if (idx >= total) return;
+    const int limb = (int)((idx % ((uint64_t)L << (2 * log_n))) >> (2 * log_n));
+    uint64_t seed = 123456789ULL + idx;
+    seed = seed * 6364136223846793005ULL + 1442695040888963407ULL;
+    a[idx] = seed % qmu[2 * limb];
+}
+
+__device__ __forceinline__ uint64_t splitmix64(uint64_t x) {
+    x += 0x9E3779B97F4A7C15ULL;
+    x = (x ^ (x >> 30)) * 0xBF58476D1CE4E5B9ULL;
+    x = (x ^ (x >> 27)) * 0x94D049BB133111EBULL;
+    return x ^ (x >> 31);
+}
+
+// gaussian_noise_kernel HE.cu:581-627: one centred sample per [w][y][x], same integer in every limb
+__global__ void gaussian_kernel(uint64_t* e, const uint64_t* qmu, int L, int log_n, uint64_t total) {
+    const uint64_t idx = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x;
+    if (idx >= total) return;
+    const uint64_t n2 = 1ull << (2 * log_n), single = (uint64_t)L * n2;
+    const uint64_t w = idx / single, off = idx % single;
+    const int limb = (int)(off / n2);
+    const uint64_t pos = off % n2;
+    const uint64_t r1 = splitmix64(0xD6E8FEB86659FD93ULL ^ (w * n2 + pos));
+    const uint64_t r2 = splitmix64(r1);
+    const double inv53 = 1.0 / 9007199254740992.0;
+    const double u1 = ((double)(r1 >> 11) + 1.0) * inv53;
+    const double u2 = ((double)(r2 >> 11) + 1.0) * inv53;
+    const double mag = 3.2 * sqrt(-2.0 * log(u1));
+    const double z = mag * cos(6.283185307179586 * u2);
+    const long long nz = llround(z);
+    const uint64_t q = qmu[2 * limb];
+    e[idx] = (nz >= 0) ? (uint64_t)nz : q - (uint64_t)(-nz);
+}
+
+// ---------------- ring ops (poly-major [phi*n][L][n]) ----------------
+// pointwise_mul_s_kernel HE.cu:509-531: t = a * s[w][l][x], w = poly / n
+__global__ void mul_s_kernel(const uint64_t* a, const uint64_t* s, uint64_t* t, const uint64_t* qmu, int L, int log_n,
+                             uint64_t total) {
+    const uint64_t idx = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x;
+    if (idx >= total) return;
+    const uint64_t n = 1ull << log_n, single = (uint64_t)L * n;
+    const uint64_t off = idx % single, poly = idx / single;
+    const int l = (int)(off >> log_n);
+    const uint64_t coeff = off & (n - 1), w = poly >> log_n;
+    const uint64_t q = qmu[2 * l];
+    const unsigned __int128 pr = (unsigned __int128)a[idx] * s[(w * L + l) * n + coeff];
+    t[idx] = (uint64_t)(pr % q);
+}
+
+// combine_b_kernel HE.cu:535-547 (b = m - t + e) and add_poly_kernel HE.cu:549-560 (b + t)
+__global__ void combine_kernel(const uint64_t* m, const uint64_t* t, const uint64_t* e, uint64_t* b,
+                               const uint64_t* qmu, int L, int log_n, uint64_t total, int add) {
+    const uint64_t idx = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x;
+    if (idx >= total) return;
+    const int l = (int)((idx % ((uint64_t)L << log_n)) >> log_n);
+    const uint64_t q = qmu[2 * l];
+    if (add) {
+        const uint64_t s = m[idx] + t[idx];
+        b[idx] = s >= q ? s - q : s;
+    } else {
+        uint64_t d = m[idx] >= t[idx] ? m[idx] - t[idx] : m[idx] + q - t[idx];
+        d += e[idx];
+        b[idx] = d >= q ? d - q : d;
+    }
+}
+
+// centred int64 -> RNS matrix-major (centered_int_to_rns_matrix_kernel HE.cu:815-835)
+__global__ void centered_to_rns_kernel(const int64_t* in, uint64_t* out, const uint64_t* qmu, int L, uint64_t n2,
+                                       uint64_t total) {
+    const uint64_t idx = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x;
+    if (idx >= total) return;
+    const uint64_t pos = idx % n2, t = idx / n2;
+    const int l = (int)(t % L);
+    const uint64_t w = t / L;
+    const int64_t v = in[w * n2 + pos];
+    const int64_t q = (int64_t)qmu[2 * l];
+    int64_t r = v % q;
+    if (r < 0) r += q;
+    out[idx] = (uint64_t)r;
+}
+
+// he_big_to_i64_checked HE.cu:904-915 over compose output
+__global__ void big_to_i64_kernel(const uint64_t* mag, const uint8_t* neg, int W, int64_t* out, uint64_t total) {
+    const uint64_t i = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x;
+    if (i >= total) return;
+    bool over = mag[i * W] > (uint64_t)INT64_MAX;
+    for (int k = 1; k < W; ++k) over |= mag[i * W + k] != 0;
+    const bool ng = neg[i] != 0;
+    out[i] = over ? (ng ? INT64_MIN : INT64_MAX) : (ng ? -(int64_t)mag[i * W] : (int64_t)mag[i * W]);
+}
+
+// limb-0 centring after the inverse (HE.cu:1112-1113)
+__global__ void center_limb0_kernel(const uint64_t* in, int64_t* out, uint64_t q, uint64_t total) {
+    const uint64_t i = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x;
+    if (i >= total) return;
+    const uint64_t a = in[i];
+    out[i] = (a > (q >> 1)) ? (int64_t)a - (int64_t)q : (int64_t)a;
+}
+
+// ---------------- helpers ----------------
+static int need_wcrt(const mfhe_ctx* c) {
+    if (!c) return set_error(MFHE_EINVAL, "null ctx");
+    if (!(c->conv & MFHE_CONV_WCRT)) return set_error(MFHE_ENOTREADY, "context was created without MFHE_CONV_WCRT");
+    return MFHE_OK;
+}
+
+struct Geo2 {
+    int L, logn;
+    uint64_t n, n2, words, cnt;   // words = phi*L*n2 ; cnt = phi*n2
+};
+static Geo2 geo(const mfhe_ctx* c) {
+    Geo2 g;
+    g.L = c->L;
+    g.logn = c->logN;
+    g.n = c->N;
+    g.n2 = g.n * g.n;
+    g.words = (uint64_t)mfhe_ctx::PHI * g.L * g.n2;
+    g.cnt = (uint64_t)mfhe_ctx::PHI * g.n2;
+    return g;
+}
+
+static size_t ws_need(const mfhe_ctx* c) {
+    const Geo2 g = geo(c);
+    return 10 * g.words * 8 + g.cnt * (size_t)c->W * 8 + 4 * g.cnt * 16 + 2 * g.cnt + (64 << 10);
+}
+
+static int ensure_ws(mfhe_ctx* c) {
+    const size_t need = ws_need(c);
+    if (c->ws_bytes >= need) return MFHE_OK;
+    if (c->ws) MFHE_HIP(hipFree(c->ws));
+    c->ws = nullptr;
+    c->ws_bytes = 0;
+    MFHE_HIP(hipMalloc(&c->ws, need));
+    c->ws_bytes = need;
+    return MFHE_OK;
+}
+
+struct Bump {
+    char* p;
+    template <class T>
+    T* get(size_t n) {
+        T* r = (T*)p;
+        p += ((n * sizeof(T) + 255) / 256) * 256;
+        return r;
+    }
+};
+
+// W-CRT forward: B matrix-major [r][L][pos] (or vector [r][L][x]); C in the requested layout
+enum class WOut { Poly, Matrix, Vector };
+static int wcrt_gemm(const mfhe_ctx* c, const uint64_t* A, const uint64_t* B, bool b_poly, uint64_t* C, WOut out,
+                     bool vector, hipStream_t s) {
+    const Geo2 g = geo(c);
+    ModGemmArgs a;
+    a.A = A;
+    a.aL = 512ull * 512;
+    a.M = 512;
+    a.K = 512;
+    a.qmu = c->d_rns_mu;
+    a.r64 = c->d_r64;
+    a.B = B;
+    a.C = C;
+    a.log_n = g.logn;
+    if (vector) {
+        a.P = (uint32_t)g.n;
+        a.bL = g.n; a.sbK = (uint64_t)g.L * g.n; a.sbY = 0;
+        a.cL = g.n; a.scM = (uint64_t)g.L * g.n; a.scY = 0;
+    } else {
+        a.P = (uint32_t)g.n2;
+        if (b_poly) { a.bL = g.n; a.sbK = g.n * g.L * g.n; a.sbY = (uint64_t)g.L * g.n; }
+        else { a.bL = g.n2; a.sbK = (uint64_t)g.L * g.n2; a.sbY = g.n; }
+        if (out == WOut::Poly) { a.cL = g.n; a.scM = g.n * g.L * g.n; a.scY = (uint64_t)g.L * g.n; }
+        else { a.cL = g.n2; a.scM = (uint64_t)g.L * g.n2; a.scY = g.n; }
+    }
+    return launch_mod_gemm(a, g.L, s);
+}
+
+// complex W-DFT / W-IDFT over [phi][n2]
+static int wdft(const mfhe_ctx* c, const double2* A, const double2* in, double2* out, hipStream_t s) {
+    const Geo2 g = geo(c);
+    CGemmArgs a;
+    a.A = A; a.B = in; a.C = out;
+    a.aB = a.bB = a.cB = 0;
+    a.M = a.K = 512;
+    a.P = (uint32_t)g.n2;
+    a.log_n = 2 * g.logn;
+    a.sbK = g.n2; a.sbY = 0; a.scM = g.n2; a.scY = 0;
+    return launch_cgemm(a, 1, s);
+}
+
+// per-lane XY: out = A * M * B over `lanes` n x n matrices (tmp: lanes*n2 complex)
+static int xy3(const mfhe_ctx* c, const double2* A, const double2* in, const double2* B, double2* tmp, double2* out,
+               size_t lanes, hipStream_t s) {
+    const Geo2 g = geo(c);
+    CGemmArgs a;
+    a.M = a.K = (int)g.n;
+    a.P = (uint32_t)g.n;
+    a.log_n = g.logn;
+    a.sbK = g.n; a.sbY = 0; a.scM = g.n; a.scY = 0;
+    a.A = A; a.aB = 0; a.B = in; a.bB = g.n2; a.C = tmp; a.cB = g.n2;        // T = A M
+    int rc = launch_cgemm(a, (int)lanes, s);
+    if (rc) return rc;
+    a.A = tmp; a.aB = g.n2; a.B = B; a.bB = 0; a.C = out; a.cB = g.n2;       // out = T B
+    return launch_cgemm(a, (int)lanes, s);
+}
+
+static int layout(const mfhe_ctx* c, const uint64_t* in, uint64_t* out, bool to_poly, hipStream_t s) {
+    const Geo2 g = geo(c);
+    if (to_poly) hipLaunchKernelGGL(layout_kernel<true>, g1(g.words), dim3(256), 0, s, in, out, g.logn, g.L, g.words);
+    else hipLaunchKernelGGL(layout_kernel<false>, g1(g.words), dim3(256), 0, s, in, out, g.logn, g.L, g.words);
+    MFHE_CHECK_LAUNCH("layout_kernel");
+    return MFHE_OK;
+}
+
+#define RC(x) do { int _r = (x); if (_r) return _r; } while (0)
+
+static int encode_impl(mfhe_ctx* c, const double* msg, uint64_t* out_re, uint64_t* out_im, hipStream_t s) {
+    RC(need_wcrt(c));
+    if (!msg || !out_re || !out_im) return set_error(MFHE_EINVAL, "mfhe_encode: null pointer");
+    RC(ensure_ws(c));
+    const Geo2 g = geo(c);
+    Bump b{(char*)c->ws};
+    double2* xy = b.get<double2>(g.cnt);
+    double2* tmp = b.get<double2>(g.cnt);
+    uint64_t* cre = b.get<uint64_t>(g.words);
+    // 1) XY-IDFT per lane (Encoder::idft2, encoder.cu:460-467)
+    RC(xy3(c, c->d_encVi, (const double2*)msg, c->d_encViT, tmp, xy, 512, s));
+    // 2) W-IDFT (w_idft_kernel, batched_encoder.cu:104-123)
+    RC(wdft(c, c->d_wdVinv, xy, tmp, s));
+    // 3) quantize + RNS split, 4) W-CRT -> matrix-major eval (re, then im)
+    RC(mfhe_rns_decompose(c, (const double*)tmp, 2, 512, g.n2, cre, (mfhe_stream_t)s));
+    RC(wcrt_gemm(c, c->d_wV, cre, false, out_re, WOut::Matrix, false, s));
+    RC(mfhe_rns_decompose(c, (const double*)tmp + 1, 2, 512, g.n2, cre, (mfhe_stream_t)s));
+    RC(wcrt_gemm(c, c->d_wV, cre, false, out_im, WOut::Matrix, false, s));
+    return MFHE_OK;
+}
+
+static int decode_impl(mfhe_ctx* c, const uint64_t* ev_re, const uint64_t* ev_im, double* msg, hipStream_t s,
+                       Bump* pb = nullptr) {
+    RC(need_wcrt(c));
+    if (!ev_re || !ev_im || !msg) return set_error(MFHE_EINVAL, "mfhe_decode: null pointer");
+    Bump b0{(char*)c->ws};
+    if (!pb) {
+        RC(ensure_ws(c));
+        pb = &b0;
+    }
+    const Geo2 g = geo(c);
+    uint64_t* coeff = pb->get<uint64_t>(g.words);
+    double2* ccx = pb->get<double2>(g.cnt);
+    double2* ecx = pb->get<double2>(g.cnt);
+    // W-INTT (poly-major in -> matrix-major coeff), CRT compose + centre + /delta fused, into re / im
+    RC(wcrt_gemm(c, c->d_wVinv, ev_re, true, coeff, WOut::Matrix, false, s));
+    RC(mfhe_crt_compose_f64(c, coeff, 512, g.n2, (double*)ccx, 2, (mfhe_stream_t)s));
+    RC(wcrt_gemm(c, c->d_wVinv, ev_im, true, coeff, WOut::Matrix, false, s));
+    RC(mfhe_crt_compose_f64(c, coeff, 512, g.n2, (double*)ccx + 1, 2, (mfhe_stream_t)s));
+    // W-DFT, then XY-DFT per lane: M = V E V^T
+    RC(wdft(c, c->d_wdV, ccx, ecx, s));
+    RC(xy3(c, c->d_encV, ecx, c->d_encVT, ccx, (double2*)msg, 512, s));
+    return MFHE_OK;
+}
+
+static int keygen_impl(mfhe_ctx* c, uint64_t* sk, hipStream_t s) {
+    RC(need_wcrt(c));
+    if (!(c->conv & MFHE_CONV_PHANTOM)) return set_error(MFHE_ENOTREADY, "keygen needs MFHE_CONV_PHANTOM (X-NTT)");
+    if (!sk) return set_error(MFHE_EINVAL, "mfhe_keygen: null pointer");
+    RC(ensure_ws(c));
+    const Geo2 g = geo(c);
+    Bump b{(char*)c->ws};
+    uint64_t* sc = b.get<uint64_t>(512ull * g.L * g.n);
+    const uint64_t total = 512ull * g.L * g.n;
+    hipLaunchKernelGGL(ternary_kernel, g1(total), dim3(256), 0, s, sc, c->d_rns_mu, g.L, g.logn, total);
+    MFHE_CHECK_LAUNCH("ternary_kernel");
+    RC(wcrt_gemm(c, c->d_wV, sc, false, sk, WOut::Vector, true, s));
+    return mfhe_ntt_fwd(c, sk, 512, 0, g.L, (mfhe_stream_t)s);
+}
+
+// encrypt (HE.cu:1370-1453) / encrypt_pair (HE.cu:1455-1552)
+static int encrypt_impl(mfhe_ctx* c, const uint64_t* m_re, const uint64_t* m_im, const uint64_t* sk, uint64_t* ct_re,
+                        uint64_t* ct_im, hipStream_t s) {
+    RC(need_wcrt(c));
+    if (!(c->conv & MFHE_CONV_PHANTOM)) return set_error(MFHE_ENOTREADY, "encrypt needs MFHE_CONV_PHANTOM (X-NTT)");
+    if (!m_re || !sk || !ct_re || (m_im && !ct_im)) return set_error(MFHE_EINVAL, "mfhe_encrypt: null pointer");
+    RC(ensure_ws(c));
+    const Geo2 g = geo(c);
+    Bump b{(char*)c->ws};
+    uint64_t* mp = b.get<uint64_t>(g.words);
+    uint64_t* ap = b.get<uint64_t>(g.words);
+    uint64_t* aev = b.get<uint64_t>(g.words);
+    uint64_t* ant = b.get<uint64_t>(g.words);
+    uint64_t* ep = b.get<uint64_t>(g.words);
+    uint64_t* eev = b.get<uint64_t>(g.words);
+    const uint64_t W = g.words;
+    // shared a: W coeff -> W-CRT eval (poly-major) -> X-NTT
+    hipLaunchKernelGGL(uniform_kernel, g1(W), dim3(256), 0, s, ap, c->d_rns_mu, g.L, g.logn, W);
+    MFHE_CHECK_LAUNCH("uniform_kernel");
+    RC(wcrt_gemm(c, c->d_wV, ap, false, aev, WOut::Poly, false, s));
+    MFHE_HIP(hipMemcpyAsync(ant, aev, W * 8, hipMemcpyDeviceToDevice, s));
+    RC(mfhe_ntt_fwd(c, ant, 512 * g.n, 0, g.L, (mfhe_stream_t)s));
+    // e: identical for re and im (seed depends only on the coefficient, HE.cu:605-608)
+    hipLaunchKernelGGL(gaussian_kernel, g1(W), dim3(256), 0, s, ep, c->d_rns_mu, g.L, g.logn, W);
+    MFHE_CHECK_LAUNCH("gaussian_kernel");
+    RC(wcrt_gemm(c, c->d_wV, ep, false, eev, WOut::Poly, false, s));
+    // t = INTT(a_ntt * s)  (reuse ep as t)
+    uint64_t* t = ep;
+    hipLaunchKernelGGL(mul_s_kernel, g1(W), dim3(256), 0, s, ant, sk, t, c->d_rns_mu, g.L, g.logn, W);
+    MFHE_CHECK_LAUNCH("mul_s_kernel");
+    RC(mfhe_ntt_inv(c, t, 512 * g.n, 0, g.L, (mfhe_stream_t)s));
+    const uint64_t* ms[2] = {m_re, m_im};
+    uint64_t* cts[2] = {ct_re, ct_im};
+    for (int k = 0; k < 2; ++k) {
+        if (!ms[k]) continue;
+        RC(layout(c, ms[k], mp, true, s));
+        hipLaunchKernelGGL(combine_kernel, g1(W), dim3(256), 0, s, mp, t, eev, ant /*b poly*/, c->d_rns_mu, g.L,
+                           g.logn, W, 0);
+        MFHE_CHECK_LAUNCH("combine_kernel");
+        RC(layout(c, ant, cts[k], false, s));          // b
+        RC(layout(c, aev, cts[k] + W, false, s));      // a (shared)
+    }
+    return MFHE_OK;
+}
+
+static int decrypt_impl(mfhe_ctx* c, const uint64_t* ct, const uint64_t* sk, uint64_t* out, hipStream_t s, Bump* pb) {
+    const Geo2 g = geo(c);
+    const uint64_t W = g.words;
+    uint64_t* bp = pb->get<uint64_t>(W);
+    uint64_t* ap = pb->get<uint64_t>(W);
+    uint64_t* t = pb->get<uint64_t>(W);
+    RC(layout(c, ct, bp, true, s));
+    RC(layout(c, ct + W, ap, true, s));
+    RC(mfhe_ntt_fwd(c, ap, 512 * g.n, 0, g.L, (mfhe_stream_t)s));
+    hipLaunchKernelGGL(mul_s_kernel, g1(W), dim3(256), 0, s, ap, sk, t, c->d_rns_mu, g.L, g.logn, W);
+    MFHE_CHECK_LAUNCH("mul_s_kernel");
+    RC(mfhe_ntt_inv(c, t, 512 * g.n, 0, g.L, (mfhe_stream_t)s));
+    hipLaunchKernelGGL(combine_kernel, g1(W), dim3(256), 0, s, bp, t, nullptr, out, c->d_rns_mu, g.L, g.logn, W, 1);
+    MFHE_CHECK_LAUNCH("combine_kernel");
+    return MFHE_OK;
+}
+
+}  // namespace mfhe
+
+using namespace mfhe;
+
+extern "C" int mfhe_ctx_reserve_workspace(mfhe_ctx* c) {
+    RC(need_wcrt(c));
+    return ensure_ws(c);
+}
+
+extern "C" int mfhe_wcrt_fwd(mfhe_ctx* c, const uint64_t* in, uint64_t* out, mfhe_stream_t s) {
+    RC(need_wcrt(c));
+    if (!in || !out) return set_error(MFHE_EINVAL, "mfhe_wcrt_fwd: null pointer");
+    return wcrt_gemm(c, c->d_wV, in, false, out, WOut::Poly, false, (hipStream_t)s);
+}
+extern "C" int mfhe_wcrt_inv(mfhe_ctx* c, const uint64_t* in, uint64_t* out, mfhe_stream_t s) {
+    RC(need_wcrt(c));
+    if (!in || !out) return set_error(MFHE_EINVAL, "mfhe_wcrt_inv: null pointer");
+    return wcrt_gemm(c, c->d_wVinv, in, true, out, WOut::Matrix, false, (hipStream_t)s);
+}
+extern "C" int mfhe_wcrt_fwd_vector(mfhe_ctx* c, const uint64_t* in, uint64_t* out, mfhe_stream_t s) {
+    RC(need_wcrt(c));
+    if (!in || !out) return set_error(MFHE_EINVAL, "mfhe_wcrt_fwd_vector: null pointer");
+    return wcrt_gemm(c, c->d_wV, in, false, out, WOut::Vector, true, (hipStream_t)s);
+}
+
+extern "C" int mfhe_wcrt_fwd_centered(mfhe_ctx* c, const int64_t* in, int64_t* out, mfhe_stream_t s_) {
+    RC(need_wcrt(c));
+    if (!in || !out) return set_error(MFHE_EINVAL, "mfhe_wcrt_fwd_centered: null pointer");
+    RC(ensure_ws(c));
+    hipStream_t s = (hipStream_t)s_;
+    const Geo2 g = geo(c);
+    Bump b{(char*)c->ws};
+    uint64_t* rns = b.get<uint64_t>(g.words);
+    uint64_t* ev = b.get<uint64_t>(g.words);
+    uint64_t* mag = b.get<uint64_t>(g.cnt * c->W);
+    uint8_t* neg = b.get<uint8_t>(g.cnt);
+    hipLaunchKernelGGL(centered_to_rns_kernel, g1(g.words), dim3(256), 0, s, in, rns, c->d_rns_mu, g.L, g.n2, g.words);
+    MFHE_CHECK_LAUNCH("centered_to_rns_kernel");
+    RC(wcrt_gemm(c, c->d_wV, rns, false, ev, WOut::Matrix, false, s));
+    RC(mfhe_crt_compose(c, ev, 512, g.n2, mag, neg, s_));
+    hipLaunchKernelGGL(big_to_i64_kernel, g1(g.cnt), dim3(256), 0, s, mag, neg, c->W, out, g.cnt);
+    MFHE_CHECK_LAUNCH("big_to_i64_kernel");
+    return MFHE_OK;
+}
+
+extern "C" int mfhe_wcrt_inv_centered(mfhe_ctx* c, const int64_t* in, int64_t* out, mfhe_stream_t s_) {
+    RC(need_wcrt(c));
+    if (!in || !out) return set_error(MFHE_EINVAL, "mfhe_wcrt_inv_centered: null pointer");
+    RC(ensure_ws(c));
+    hipStream_t s = (hipStream_t)s_;
+    const Geo2 g = geo(c);
+    Bump b{(char*)c->ws};
+    uint64_t* rns = b.get<uint64_t>(g.cnt);
+    uint64_t* co = b.get<uint64_t>(g.cnt);
+    // limb 0 only (HE.cu:1101): treat the input as a 1-limb matrix-major array
+    hipLaunchKernelGGL(centered_to_rns_kernel, g1(g.cnt), dim3(256), 0, s, in, rns, c->d_rns_mu, 1, g.n2, g.cnt);
+    MFHE_CHECK_LAUNCH("centered_to_rns_kernel");
+    ModGemmArgs a;
+    a.A = c->d_wVinv; a.aL = 0; a.M = a.K = 512; a.qmu = c->d_rns_mu; a.r64 = c->d_r64;
+    a.B = rns; a.bL = 0; a.sbK = g.n2; a.sbY = g.n; a.log_n = g.logn; a.P = (uint32_t)g.n2;
+    a.C = co; a.cL = 0; a.scM = g.n2; a.scY = g.n;
+    RC(launch_mod_gemm(a, 1, s));
+    hipLaunchKernelGGL(center_limb0_kernel, g1(g.cnt), dim3(256), 0, s, co, out, c->moduli[0], g.cnt);
+    MFHE_CHECK_LAUNCH("center_limb0_kernel");
+    return MFHE_OK;
+}
+
+extern "C" int mfhe_wdft_fwd(mfhe_ctx* c, const double* in, double* out, mfhe_stream_t s) {
+    RC(need_wcrt(c));
+    if (!in || !out || in == out) return set_error(MFHE_EINVAL, "mfhe_wdft_fwd: need distinct in/out");
+    return wdft(c, c->d_wdV, (const double2*)in, (double2*)out, (hipStream_t)s);
+}
+extern "C" int mfhe_wdft_inv(mfhe_ctx* c, const double* in, double* out, mfhe_stream_t s) {
+    RC(need_wcrt(c));
+    if (!in || !out || in == out) return set_error(MFHE_EINVAL, "mfhe_wdft_inv: need distinct in/out");
+    return wdft(c, c->d_wdVinv, (const double2*)in, (double2*)out, (hipStream_t)s);
+}
+
+static int xy_entry(mfhe_ctx* c, const double* in, double* out, size_t lanes, mfhe_stream_t s, bool inv) {
+    RC(need_wcrt(c));
+    if (lanes == 0) return MFHE_OK;
+    if (!in || !out || in == out) return set_error(MFHE_EINVAL, "mfhe_xy_(i)dft: need distinct in/out");
+    if (lanes > 65535) return set_error(MFHE_EINVAL, "mfhe_xy_(i)dft: at most 65535 lanes per call");
+    RC(ensure_ws(c));
+    double2* tmp = (double2*)c->ws;
+    const Geo2 g = geo(c);
+    if (lanes * g.n2 * 16 > c->ws_bytes) return set_error(MFHE_EINVAL, "too many lanes for the workspace");
+    return inv ? xy3(c, c->d_encVi, (const double2*)in, c->d_encViT, tmp, (double2*)out, lanes, (hipStream_t)s)
+               : xy3(c, c->d_encV, (const double2*)in, c->d_encVT, tmp, (double2*)out, lanes, (hipStream_t)s);
+}
+extern "C" int mfhe_xy_idft(mfhe_ctx* c, const double* in, double* out, size_t lanes, mfhe_stream_t s) {
+    return xy_entry(c, in, out, lanes, s, true);
+}
+extern "C" int mfhe_xy_dft(mfhe_ctx* c, const double* in, double* out, size_t lanes, mfhe_stream_t s) {
+    return xy_entry(c, in, out, lanes, s, false);
+}
+
+extern "C" int mfhe_matrix_to_poly(mfhe_ctx* c, const uint64_t* in, uint64_t* out, mfhe_stream_t s) {
+    RC(need_wcrt(c));
+    if (!in || !out || in == out) return set_error(MFHE_EINVAL, "layout needs distinct in/out");
+    return layout(c, in, out, true, (hipStream_t)s);
+}
+extern "C" int mfhe_poly_to_matrix(mfhe_ctx* c, const uint64_t* in, uint64_t* out, mfhe_stream_t s) {
+    RC(need_wcrt(c));
+    if (!in || !out || in == out) return set_error(MFHE_EINVAL, "layout needs distinct in/out");
+    return layout(c, in, out, false, (hipStream_t)s);
+}
+
+extern "C" int mfhe_encode(mfhe_ctx* c, const double* msg, uint64_t* re, uint64_t* im, mfhe_stream_t s) {
+    return encode_impl(c, msg, re, im, (hipStream_t)s);
+}
+extern "C" int mfhe_decode(mfhe_ctx* c, const uint64_t* re, const uint64_t* im, double* msg, mfhe_stream_t s) {
+    return decode_impl(c, re, im, msg, (hipStream_t)s);
+}
+extern "C" int mfhe_keygen(mfhe_ctx* c, uint64_t* sk, mfhe_stream_t s) { return keygen_impl(c, sk, (hipStream_t)s); }
+extern "C" int mfhe_encrypt(mfhe_ctx* c, const uint64_t* m, const uint64_t* sk, uint64_t* ct, mfhe_stream_t s) {
+    return encrypt_impl(c, m, nullptr, sk, ct, nullptr, (hipStream_t)s);
+}
+extern "C" int mfhe_encrypt_pair(mfhe_ctx* c, const uint64_t* mre, const uint64_t* mim, const uint64_t* sk,
+                                 uint64_t* cre, uint64_t* cim, mfhe_stream_t s) {
+    if (!mim || !cim) return set_error(MFHE_EINVAL, "mfhe_encrypt_pair: null pointer");
+    return encrypt_impl(c, mre, mim, sk, cre, cim, (hipStream_t)s);
+}
+extern "C" int mfhe_decrypt_to_eval(mfhe_ctx* c, const uint64_t* ct, const uint64_t* sk, uint64_t* out,
+                                    mfhe_stream_t s) {
+    RC(need_wcrt(c));
+    if (!(c->conv & MFHE_CONV_PHANTOM)) return set_error(MFHE_ENOTREADY, "decrypt needs MFHE_CONV_PHANTOM (X-NTT)");
+    if (!ct || !sk || !out) return set_error(MFHE_EINVAL, "mfhe_decrypt_to_eval: null pointer");
+    RC(ensure_ws(c));
+    Bump b{(char*)c->ws};
+    return decrypt_impl(c, ct, sk, out, (hipStream_t)s, &b);
+}
+extern "C" int mfhe_decrypt_and_decode(mfhe_ctx* c, const uint64_t* cre, const uint64_t* cim, const uint64_t* sk,
+                                       double* msg, mfhe_stream_t s) {
+    RC(need_wcrt(c));
+    if (!(c->conv & MFHE_CONV_PHANTOM)) return set_error(MFHE_ENOTREADY, "decrypt needs MFHE_CONV_PHANTOM (X-NTT)");
+    if (!cre || !cim || !sk || !msg) return set_error(MFHE_EINVAL, "mfhe_decrypt_and_decode: null pointer");
+    RC(ensure_ws(c));
+    const Geo2 g = geo(c);
+    Bump b{(char*)c->ws};
+    uint64_t* er = b.get<uint64_t>(g.words);
+    uint64_t* ei = b.get<uint64_t>(g.words);
+    Bump inner = b;
+    RC(decrypt_impl(c, cre, sk, er, (hipStream_t)s, &inner));
+    inner = b;
+    RC(decrypt_impl(c, cim, sk, ei, (hipStream_t)s, &inner));
+    inner = b;
+    return decode_impl(c, er, ei, msg, (hipStream_t)s, &inner);
+}

@@ -1,6 +1,10 @@
 // host_math.cpp -- see host_math.hpp.
 #include "host_math.hpp"
 
+#include <algorithm>
+#include <complex>
+#include <thread>
+
 namespace mfhe {
 namespace hm {
 
@@ -66,6 +70,80 @@ uint64_t find_eta771(uint64_t q) {
         return eta;
     }
     return 0;
+}
+
+void wcrt_exponents(uint16_t* exp512) {
+    int idx = 0;
+    for (int a = 1; a <= 2; ++a)
+        for (int b = 1; b <= 256; ++b) exp512[idx++] = (uint16_t)((a * 257 + b * 3) % 771);
+}
+
+bool vandermonde_inverse_mod(const std::vector<uint64_t>& x, uint64_t q, std::vector<uint64_t>& inv) {
+    const int dim = (int)x.size();
+    inv.assign((size_t)dim * dim, 0);
+    std::vector<uint64_t> P((size_t)dim + 1, 0);   // P(X) = prod (X - x_j)
+    P[0] = 1;
+    for (int j = 0; j < dim; ++j) {
+        const uint64_t nx = (q - x[j]) % q;
+        for (int k = j + 1; k >= 1; --k) P[k] = addmod(P[k - 1], mulmod(P[k], nx, q), q);
+        P[0] = mulmod(P[0], nx, q);
+    }
+    bool ok = true;
+    std::vector<uint64_t> b(dim);
+    for (int w = 0; w < dim; ++w) {   // synthetic division P / (X - x_w), then P'(x_w)
+        b[dim - 1] = P[dim];
+        for (int k = dim - 1; k >= 1; --k) b[k - 1] = addmod(mulmod(x[w], b[k], q), P[k], q);
+        uint64_t den = 0;
+        for (int k = dim - 1; k >= 0; --k) den = addmod(mulmod(den, x[w], q), b[k], q);
+        if (den == 0) { ok = false; continue; }
+        const uint64_t di = invmod(den, q);
+        for (int r = 0; r < dim; ++r) inv[(size_t)r * dim + w] = mulmod(b[r], di, q);
+    }
+    return ok;
+}
+
+bool complex_inverse_gj(std::vector<double>& a_ri, int dim, std::vector<double>& inv_ri) {
+    using C = std::complex<double>;
+    C* a = reinterpret_cast<C*>(a_ri.data());
+    inv_ri.assign((size_t)dim * dim * 2, 0.0);
+    C* inv = reinterpret_cast<C*>(inv_ri.data());
+    for (int i = 0; i < dim; ++i) inv[(size_t)i * dim + i] = 1.0;
+    const unsigned nth = std::max(1u, std::min(16u, std::thread::hardware_concurrency()));
+    for (int i = 0; i < dim; ++i) {
+        int piv = i;
+        double best = std::abs(a[(size_t)i * dim + i]);
+        for (int r = i + 1; r < dim; ++r) {
+            const double cand = std::abs(a[(size_t)r * dim + i]);
+            if (cand > best) { best = cand; piv = r; }
+        }
+        if (best < 1e-18) return false;
+        if (piv != i)
+            for (int j = 0; j < dim; ++j) {
+                std::swap(a[(size_t)i * dim + j], a[(size_t)piv * dim + j]);
+                std::swap(inv[(size_t)i * dim + j], inv[(size_t)piv * dim + j]);
+            }
+        const C pv = a[(size_t)i * dim + i];
+        for (int j = 0; j < dim; ++j) { a[(size_t)i * dim + j] /= pv; inv[(size_t)i * dim + j] /= pv; }
+        auto work = [&](int r0, int r1) {
+            for (int r = r0; r < r1; ++r) {
+                if (r == i) continue;
+                const C f = a[(size_t)r * dim + i];
+                if (std::abs(f) < 1e-18) continue;
+                for (int c = 0; c < dim; ++c) {
+                    a[(size_t)r * dim + c] -= f * a[(size_t)i * dim + c];
+                    inv[(size_t)r * dim + c] -= f * inv[(size_t)i * dim + c];
+                }
+            }
+        };
+        std::vector<std::thread> th;
+        const int chunk = (dim + (int)nth - 1) / (int)nth;
+        for (unsigned t = 0; t < nth; ++t) {
+            const int r0 = (int)t * chunk, r1 = std::min(dim, r0 + chunk);
+            if (r0 < r1) th.emplace_back(work, r0, r1);
+        }
+        for (auto& t : th) t.join();
+    }
+    return true;
 }
 
 void big_mul_u64(const uint64_t* a, uint64_t m, uint64_t* out, int W) {

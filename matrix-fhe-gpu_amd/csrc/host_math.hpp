@@ -45,6 +45,15 @@ uint64_t first_psi4n(uint64_t q, uint64_t n);
 // reference h_find_eta (HE.cu:119-133); 0 if none
 uint64_t find_eta771(uint64_t q);
 
+// exp[] order of the 512 W lanes (HE.cu:72-105 == batched_encoder.cu:276-282): a*257 + b*3 mod 771
+void wcrt_exponents(uint16_t* exp512);
+// Exact inverse of the Vandermonde matrix V[w][r] = x_w^r mod q (dim x dim, row-major out[r][w]) by
+// Lagrange interpolation, O(dim^2).  Equal to the reference's Gauss-Jordan inverse (HE.cu:135-185),
+// the inverse being unique.  Returns false if two points coincide.
+bool vandermonde_inverse_mod(const std::vector<uint64_t>& x, uint64_t q, std::vector<uint64_t>& inv);
+// Complex Gauss-Jordan with partial pivoting (matrix_inverse_complex, HE.cu:187-235); row-major, in place.
+bool complex_inverse_gj(std::vector<double>& a_ri, int dim, std::vector<double>& inv_ri);
+
 // multiprecision helpers, little-endian words
 void big_mul_u64(const uint64_t* a, uint64_t m, uint64_t* out, int W);
 int bitlen(const std::vector<uint64_t>& a);

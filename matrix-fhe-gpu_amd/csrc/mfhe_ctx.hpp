@@ -83,6 +83,19 @@ struct mfhe_ctx {
     uint64_t* d_crt_Q = nullptr;      // [W]
     uint64_t* d_crt_Qhalf = nullptr;  // [W]
     uint64_t* d_rns_mu = nullptr;     // [L][2] (q, floor(2^64/q))
+    uint64_t* d_r64 = nullptr;        // [L]     2^64 mod q
+
+    // W axis (MFHE_CONV_WCRT), phi = 512
+    static constexpr int PHI = 512;
+    uint64_t* d_wV = nullptr;      // [L][512][512]  V_l[w][r]
+    uint64_t* d_wVinv = nullptr;   // [L][512][512]  V_l^-1[r][w] (row-major)
+    double2* d_wdV = nullptr;      // [512][512]     complex W-DFT
+    double2* d_wdVinv = nullptr;   // [512][512]     its inverse (complex Gauss-Jordan)
+    double2 *d_encV = nullptr, *d_encVT = nullptr, *d_encVi = nullptr, *d_encViT = nullptr;  // [n][n]
+
+    // pipeline workspace (allocated on first use / mfhe_ctx_reserve_workspace)
+    void* ws = nullptr;
+    size_t ws_bytes = 0;
 
     std::vector<void*> allocs;  // everything above, freed at destroy
 };

@@ -89,6 +89,19 @@ _sig("mfhe_rns_decompose", [_vp, _vp, _sz, _sz, _sz, _vp, _vp])
 _sig("mfhe_crt_compose", [_vp, _vp, _sz, _sz, _vp, _vp, _vp])
 _sig("mfhe_crt_to_f64", [_vp, _vp, _vp, _sz, _vp, _sz, _vp])
 _sig("mfhe_crt_compose_f64", [_vp, _vp, _sz, _sz, _vp, _sz, _vp])
+for _n in ("mfhe_wcrt_fwd", "mfhe_wcrt_inv", "mfhe_wcrt_fwd_vector", "mfhe_wcrt_fwd_centered",
+           "mfhe_wcrt_inv_centered", "mfhe_wdft_fwd", "mfhe_wdft_inv", "mfhe_matrix_to_poly", "mfhe_poly_to_matrix",
+           "mfhe_keygen"):
+    _sig(_n, [_vp, _vp, _vp, _vp] if _n != "mfhe_keygen" else [_vp, _vp, _vp])
+_sig("mfhe_xy_idft", [_vp, _vp, _vp, _sz, _vp])
+_sig("mfhe_xy_dft", [_vp, _vp, _vp, _sz, _vp])
+_sig("mfhe_ctx_reserve_workspace", [_vp])
+_sig("mfhe_encode", [_vp, _vp, _vp, _vp, _vp])
+_sig("mfhe_decode", [_vp, _vp, _vp, _vp, _vp])
+_sig("mfhe_encrypt", [_vp, _vp, _vp, _vp, _vp])
+_sig("mfhe_encrypt_pair", [_vp, _vp, _vp, _vp, _vp, _vp, _vp])
+_sig("mfhe_decrypt_to_eval", [_vp, _vp, _vp, _vp, _vp])
+_sig("mfhe_decrypt_and_decode", [_vp, _vp, _vp, _vp, _vp, _vp])
 _sig("mfhe_last_error", [], ctypes.c_char_p)
 _sig("mfhe_version", [], ctypes.c_char_p)
 
@@ -233,6 +246,44 @@ class Context:
         check(lib.mfhe_crt_compose_f64(self._h, _ptr(src), npoly, ncoeff, _ptr(out), out_stride, _stream_ptr(stream)),
               "crt_compose_f64")
         return out
+
+
+    # ---- W axis / encoder / pipelines (reference geometry, CONV_WCRT) ----
+    def _call(self, name, *ptrs, stream=None):
+        fn = getattr(lib, name)
+        check(fn(self._h, *ptrs, _stream_ptr(stream)), name)
+
+    def wcrt_fwd(self, src, dst, stream=None): self._call("mfhe_wcrt_fwd", _ptr(src), _ptr(dst), stream=stream); return dst
+    def wcrt_inv(self, src, dst, stream=None): self._call("mfhe_wcrt_inv", _ptr(src), _ptr(dst), stream=stream); return dst
+    def wcrt_fwd_vector(self, src, dst, stream=None):
+        self._call("mfhe_wcrt_fwd_vector", _ptr(src), _ptr(dst), stream=stream); return dst
+    def wcrt_fwd_centered(self, src, dst, stream=None):
+        self._call("mfhe_wcrt_fwd_centered", _ptr(src), _ptr(dst), stream=stream); return dst
+    def wcrt_inv_centered(self, src, dst, stream=None):
+        self._call("mfhe_wcrt_inv_centered", _ptr(src), _ptr(dst), stream=stream); return dst
+    def wdft_fwd(self, src, dst, stream=None): self._call("mfhe_wdft_fwd", _ptr(src), _ptr(dst), stream=stream); return dst
+    def wdft_inv(self, src, dst, stream=None): self._call("mfhe_wdft_inv", _ptr(src), _ptr(dst), stream=stream); return dst
+    def xy_dft(self, src, dst, lanes, stream=None):
+        check(lib.mfhe_xy_dft(self._h, _ptr(src), _ptr(dst), lanes, _stream_ptr(stream)), "xy_dft"); return dst
+    def xy_idft(self, src, dst, lanes, stream=None):
+        check(lib.mfhe_xy_idft(self._h, _ptr(src), _ptr(dst), lanes, _stream_ptr(stream)), "xy_idft"); return dst
+    def matrix_to_poly(self, src, dst, stream=None):
+        self._call("mfhe_matrix_to_poly", _ptr(src), _ptr(dst), stream=stream); return dst
+    def poly_to_matrix(self, src, dst, stream=None):
+        self._call("mfhe_poly_to_matrix", _ptr(src), _ptr(dst), stream=stream); return dst
+    def reserve_workspace(self): check(lib.mfhe_ctx_reserve_workspace(self._h), "reserve_workspace")
+    def encode(self, msg, out_re, out_im, stream=None):
+        self._call("mfhe_encode", _ptr(msg), _ptr(out_re), _ptr(out_im), stream=stream)
+    def decode(self, ev_re, ev_im, msg, stream=None):
+        self._call("mfhe_decode", _ptr(ev_re), _ptr(ev_im), _ptr(msg), stream=stream); return msg
+    def keygen(self, sk, stream=None): self._call("mfhe_keygen", _ptr(sk), stream=stream); return sk
+    def encrypt(self, m, sk, ct, stream=None): self._call("mfhe_encrypt", _ptr(m), _ptr(sk), _ptr(ct), stream=stream)
+    def encrypt_pair(self, m_re, m_im, sk, ct_re, ct_im, stream=None):
+        self._call("mfhe_encrypt_pair", _ptr(m_re), _ptr(m_im), _ptr(sk), _ptr(ct_re), _ptr(ct_im), stream=stream)
+    def decrypt_to_eval(self, ct, sk, out, stream=None):
+        self._call("mfhe_decrypt_to_eval", _ptr(ct), _ptr(sk), _ptr(out), stream=stream); return out
+    def decrypt_and_decode(self, ct_re, ct_im, sk, msg, stream=None):
+        self._call("mfhe_decrypt_and_decode", _ptr(ct_re), _ptr(ct_im), _ptr(sk), _ptr(msg), stream=stream); return msg
 
 
 def fnwt_1d(data, tw, tw_shoup, dmod, dim, coeff_modulus_size, start_modulus_idx=0, batch=1, stream=None):
