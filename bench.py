@@ -38,7 +38,9 @@ def parse():
     ap.add_argument("--arith", type=int, default=0, help="0 auto, 1 f64, 2 u64")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-seconds", type=float, default=10.0)
-    ap.add_argument("--only", default="all", help="all | ntt | crt (profiling)")
+    ap.add_argument("--only", default="all", help="all | ntt | crt | recombine (profiling)")
+    ap.add_argument("--recombine-batch", type=int, default=256,
+                    help="polys per step for the residue-shard INTT + CRT recombine line (0 = skip)")
     return ap.parse_args()
 
 
@@ -177,6 +179,32 @@ def main():
         wall_c, ev_c = timed(enc_crt, max(1, args.steps // 2), 1)
         res["crt_ev_ms"], res["crt_batch"] = ev_c, cb
 
+    if args.only in ("all", "recombine") and args.recombine_batch and L % world == 0:
+        # residue sharding: rank g owns limbs [g*L/G, (g+1)*L/G) of every poly; one step =
+        # INTT of the shard + RCCL exchange + sharded CRT compose of this rank's batch slice -> f64.
+        from mfhe import dist as mdist
+        rb = max(world, args.recombine_batch // world * world)
+        s0, lg = mdist.limb_range(L, world, rank)
+        shard = torch.empty(rb * lg * N, dtype=torch.int64, device=dev).random_(0, 2 ** 62, generator=g)
+        shard.remainder_(torch.tensor(moduli[s0:s0 + lg], dtype=torch.int64, device=dev).repeat_interleave(N).repeat(rb))
+        rout = torch.empty(rb // world * N, dtype=torch.float64, device=dev)
+        rc = {}
+        modes = ("allgather", "alltoall") if world > 1 else ("local",)
+        for mode in modes:
+            def step(mode=mode):
+                ctx.ntt_inv(shard, batch=rb, start_limb=s0, nlimbs=lg, stream=stream)
+                if mode == "local":
+                    ctx.crt_compose_f64(shard, rout, rb, N, stream=stream)
+                else:
+                    mdist.crt_recombine(ctx, shard, rb, N, mode, out=rout, stream=stream)
+            w_r, ev_r = timed(step, max(1, args.steps // 4), 1)
+            rc[mode] = w_r / max(1, args.steps // 4)
+        w_n, _ = timed(lambda: ctx.ntt_inv(shard, batch=rb, start_limb=s0, nlimbs=lg, stream=stream),
+                       max(1, args.steps // 4), 1)
+        res["recombine"] = {"batch": rb, "limbs_per_gpu": lg, "intt_only_ms": w_n / max(1, args.steps // 4) * 1e3,
+                            **{f"{m}_ms": t * 1e3 for m, t in rc.items()},
+                            **{f"{m}_polys_per_s": rb / t for m, t in rc.items()}}
+
     if rank == 0:
         ntts = batch * L * world
         out = {
@@ -213,6 +241,8 @@ def main():
             cb = res["crt_batch"]
             out["encode_crt_ops_per_s"] = cb / (res["crt_ev_ms"] * 1e-3) * world
             out["encode_crt_GBps"] = 16.0 * (L + 1) * N * cb / (res["crt_ev_ms"] * 1e-3) / 1e9
+        if "recombine" in res:
+            out["residue_shard_intt_crt_recombine"] = res["recombine"]
         if world == 1 and not args.no_cpu_baseline and args.only == "all":
             try:
                 out["cpu_baseline"] = cpu_baseline(log_n, moduli, args.cpu_seconds)

@@ -44,19 +44,26 @@ __global__ __launch_bounds__(256) void rns_decompose_kernel(const double* __rest
 }
 
 // ---------------- wide CRT compose ----------------
+// Limb k of the coefficient is read from in[(k / Lg) * shard_stride + (k % Lg) * ncoeff]: Lg = L and
+// shard_stride = 0 is the plain [npoly][L][ncoeff] layout; Lg < L reads residue shards gathered from
+// several GPUs ([shard][npoly][Lg][ncoeff]) in place, without a transpose.
 template <int W>
-__device__ __forceinline__ void compose_one(const uint64_t* __restrict__ in, uint64_t ncoeff, int L,
-                                            const uint64_t* __restrict__ qmu, const uint64_t* __restrict__ inv,
-                                            const double* __restrict__ qinv, const uint64_t* __restrict__ M,
-                                            const uint64_t* __restrict__ Q, const uint64_t* __restrict__ Qh,
-                                            uint64_t (&mag)[W], bool& neg) {
+__device__ __forceinline__ void compose_one(const uint64_t* __restrict__ in, uint64_t ncoeff, int L, int Lg,
+                                            uint64_t shard_stride, const uint64_t* __restrict__ qmu,
+                                            const uint64_t* __restrict__ inv, const double* __restrict__ qinv,
+                                            const uint64_t* __restrict__ M, const uint64_t* __restrict__ Q,
+                                            const uint64_t* __restrict__ Qh, uint64_t (&mag)[W], bool& neg) {
     uint64_t acc[W + 1];
 #pragma unroll
     for (int i = 0; i <= W; ++i) acc[i] = 0;
     double est = 0.0;
-    for (int k = 0; k < L; ++k) {
+    for (int k = 0, j = 0; k < L; ++k) {
         const uint64_t q = qmu[2 * k];
-        const uint64_t x = in[(uint64_t)k * ncoeff];
+        const uint64_t x = in[(uint64_t)j * ncoeff];
+        if (++j == Lg) {
+            j = 0;
+            in += shard_stride;
+        }
         uint64_t t = x * inv[2 * k] - __umul64hi(x, inv[2 * k + 1]) * q;   // Shoup: [0, 2q)
         t = t >= q ? t - q : t;
         est += (double)t * qinv[k];
@@ -147,7 +154,8 @@ __device__ __forceinline__ double big_to_f64(const uint64_t (&mag)[W], bool neg,
 struct CrtArgs {
     const uint64_t* in;
     uint64_t ncoeff, total;
-    int L;
+    int L, Lg;                // limbs per shard (Lg = L: unsharded)
+    uint64_t shard_stride;    // words between shards
     const uint64_t *qmu, *inv;
     const double* qinv;
     const uint64_t *M, *Q, *Qh;
@@ -161,7 +169,8 @@ __global__ __launch_bounds__(256) void crt_compose_kernel(CrtArgs a, uint64_t* _
     const uint64_t p = i / a.ncoeff, c = i - p * a.ncoeff;
     uint64_t mag[W];
     bool neg;
-    compose_one<W>(a.in + p * (uint64_t)a.L * a.ncoeff + c, a.ncoeff, a.L, a.qmu, a.inv, a.qinv, a.M, a.Q, a.Qh, mag, neg);
+    compose_one<W>(a.in + p * (uint64_t)a.Lg * a.ncoeff + c, a.ncoeff, a.L, a.Lg, a.shard_stride, a.qmu, a.inv,
+                   a.qinv, a.M, a.Q, a.Qh, mag, neg);
     uint64_t* o = out_mag + i * W;
 #pragma unroll
     for (int w = 0; w < W; ++w) o[w] = mag[w];
@@ -176,7 +185,8 @@ __global__ __launch_bounds__(256) void crt_compose_f64_kernel(CrtArgs a, double 
     const uint64_t p = i / a.ncoeff, c = i - p * a.ncoeff;
     uint64_t mag[W];
     bool neg;
-    compose_one<W>(a.in + p * (uint64_t)a.L * a.ncoeff + c, a.ncoeff, a.L, a.qmu, a.inv, a.qinv, a.M, a.Q, a.Qh, mag, neg);
+    compose_one<W>(a.in + p * (uint64_t)a.Lg * a.ncoeff + c, a.ncoeff, a.L, a.Lg, a.shard_stride, a.qmu, a.inv,
+                   a.qinv, a.M, a.Q, a.Qh, mag, neg);
     out[i * out_stride] = big_to_f64<W>(mag, neg, delta);
 }
 
@@ -202,6 +212,8 @@ static CrtArgs crt_args(const mfhe_ctx* c, const uint64_t* in, uint64_t npoly, u
     a.ncoeff = ncoeff;
     a.total = npoly * ncoeff;
     a.L = c->L;
+    a.Lg = c->L;
+    a.shard_stride = 0;
     a.qmu = c->d_rns_mu;
     a.inv = c->d_crt_inv;
     a.qinv = c->d_crt_qinv;
@@ -284,5 +296,30 @@ extern "C" int mfhe_crt_to_f64(mfhe_ctx* c, const uint64_t* mag, const uint8_t* 
         default: return set_error(MFHE_EUNSUPPORTED, "crt words > 32");
     }
     MFHE_CHECK_LAUNCH("crt_to_f64_kernel");
+    return MFHE_OK;
+}
+
+extern "C" int mfhe_crt_compose_f64_sharded(mfhe_ctx* c, const uint64_t* in, int nshards, size_t shard_stride,
+                                            size_t npoly, size_t ncoeff, double* out, size_t out_stride,
+                                            mfhe_stream_t s) {
+    if (!c) return set_error(MFHE_EINVAL, "null ctx");
+    if (nshards < 1 || c->L % nshards) return set_error(MFHE_EINVAL, "mfhe_crt_compose_f64_sharded: nshards must divide L");
+    const uint64_t total = (uint64_t)npoly * ncoeff;
+    if (total == 0) return MFHE_OK;
+    if (!in || !out || out_stride == 0) return set_error(MFHE_EINVAL, "mfhe_crt_compose_f64_sharded: bad pointer/stride");
+    CrtArgs a = crt_args(c, in, npoly, ncoeff);
+    a.Lg = c->L / nshards;
+    a.shard_stride = (uint64_t)shard_stride;
+    switch (c->W) {
+#define X(w)                                                                                                       \
+    case w:                                                                                                        \
+        hipLaunchKernelGGL(crt_compose_f64_kernel<w>, grid1d(total, 256), dim3(256), 0, (hipStream_t)s, a, c->delta, \
+                           out, (uint64_t)out_stride);                                                            \
+        break;
+        MFHE_W_CASES(X)
+#undef X
+        default: return set_error(MFHE_EUNSUPPORTED, "crt words > 32");
+    }
+    MFHE_CHECK_LAUNCH("crt_compose_f64_kernel");
     return MFHE_OK;
 }

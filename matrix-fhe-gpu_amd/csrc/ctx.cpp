@@ -11,6 +11,7 @@
 #include <algorithm>
 #include <cmath>
 #include <complex>
+#include <mutex>
 #include <thread>
 #include <cstring>
 #include <string>
@@ -124,12 +125,12 @@ static void powers(uint64_t q, uint64_t r, size_t n, bool f64, std::vector<uint6
     }
 }
 
-static int build_crt(mfhe_ctx* c) {
+static int build_crt(mfhe_ctx* c, int min_words) {
     const int L = c->L;
     std::vector<uint64_t> Q(64, 0);
     Q[0] = 1;
     for (int i = 0; i < L; ++i) hm::big_mul_u64(Q.data(), c->moduli[i], Q.data(), 64);
-    const int W = std::max(1, (hm::bitlen(Q) + 1 + 63) / 64);
+    const int W = std::max(min_words, std::max(1, (hm::bitlen(Q) + 1 + 63) / 64));
     if (W > 32) return set_error(MFHE_EUNSUPPORTED, "wide CRT needs more than 32 words (product of moduli > 2^2047)");
     c->W = W;
     Q.resize(W);
@@ -198,9 +199,13 @@ static int build_wcrt(mfhe_ctx* c) {
     for (auto& t : th) t.join();
     for (int l = 0; l < L; ++l)
         if (bad[l]) return set_error(MFHE_EUNSUPPORTED, "W-CRT table construction failed (no order-771 root)");
-    // complex W-DFT: V[w][r] = root_w^r by repeated multiplication, as HE.cu:282-290
-    std::vector<double> wd((size_t)PHI * PHI * 2), wdi;
-    {
+    // complex W-DFT: V[w][r] = root_w^r by repeated multiplication, as HE.cu:282-290.  Depends on nothing
+    // but phi, so the (0.5 s) complex Gauss-Jordan inverse is computed once per process.
+    static std::mutex wd_mu;
+    static std::vector<double> wd_cache, wdi_cache;
+    std::lock_guard<std::mutex> lk(wd_mu);
+    if (wd_cache.empty()) {
+        std::vector<double> wd((size_t)PHI * PHI * 2), wdi;
         const double p = 771.0, two_pi = 6.283185307179586476925286766559;
         for (int w = 0; w < PHI; ++w) {
             const double ang = two_pi * (double)exp[w] / p;
@@ -214,8 +219,26 @@ static int build_wcrt(mfhe_ctx* c) {
         }
         std::vector<double> a = wd;
         if (!hm::complex_inverse_gj(a, PHI, wdi)) return set_error(MFHE_EUNSUPPORTED, "W-DFT matrix singular");
+        wd_cache.swap(wd);
+        wdi_cache.swap(wdi);
     }
-    // XY encoder matrices
+    const std::vector<double>& wd = wd_cache;
+    const std::vector<double>& wdi = wdi_cache;
+    std::vector<double2> wdv((size_t)PHI * PHI), wdvi((size_t)PHI * PHI);
+    std::memcpy(wdv.data(), wd.data(), wd.size() * 8);
+    std::memcpy(wdvi.data(), wdi.data(), wdi.size() * 8);
+    int rc;
+    if ((rc = upload(c, &c->d_wV, V)) || (rc = upload(c, &c->d_wVinv, Vi)) || (rc = upload(c, &c->d_wdV, wdv)) ||
+        (rc = upload(c, &c->d_wdVinv, wdvi)))
+        return rc;
+    return MFHE_OK;
+}
+
+// XY encoder matrices: Encoder::init_complex_matrices (encoder.cu:425-444); n x n complex, built on first
+// use (they only make sense for the matrix dimension n = N of the X/Y axes, so N is capped at 2^10).
+int ensure_xy(mfhe_ctx* c) {
+    if (c->d_encV) return MFHE_OK;
+    if (c->N > 1024) return set_error(MFHE_EUNSUPPORTED, "XY encoder matrices need n <= 1024");
     const int n = (int)c->N;
     std::vector<double2> eV((size_t)n * n), eVT((size_t)n * n), eVi((size_t)n * n), eViT((size_t)n * n);
     {
@@ -242,13 +265,9 @@ static int build_wcrt(mfhe_ctx* c) {
                 eViT[(size_t)cc2 * n + r] = eVi[(size_t)r * n + cc2];
             }
     }
-    std::vector<double2> wdv((size_t)PHI * PHI), wdvi((size_t)PHI * PHI);
-    std::memcpy(wdv.data(), wd.data(), wd.size() * 8);
-    std::memcpy(wdvi.data(), wdi.data(), wdi.size() * 8);
     int rc;
-    if ((rc = upload(c, &c->d_wV, V)) || (rc = upload(c, &c->d_wVinv, Vi)) || (rc = upload(c, &c->d_wdV, wdv)) ||
-        (rc = upload(c, &c->d_wdVinv, wdvi)) || (rc = upload(c, &c->d_encV, eV)) || (rc = upload(c, &c->d_encVT, eVT)) ||
-        (rc = upload(c, &c->d_encVi, eVi)) || (rc = upload(c, &c->d_encViT, eViT)))
+    if ((rc = upload(c, &c->d_encV, eV)) || (rc = upload(c, &c->d_encVT, eVT)) || (rc = upload(c, &c->d_encVi, eVi)) ||
+        (rc = upload(c, &c->d_encViT, eViT)))
         return rc;
     return MFHE_OK;
 }
@@ -359,7 +378,7 @@ static int ctx_create_impl(const uint64_t* moduli, int L, int logN, int conv, do
         }
         if ((rc = upload(c, &c->gl_perm, perm)) || (rc = upload(c, &c->gl_inv_perm, iperm))) return fail(rc);
     }
-    if ((rc = build_crt(c))) return fail(rc);
+    if ((rc = build_crt(c, 1))) return fail(rc);
     if ((conv & MFHE_CONV_WCRT) && (rc = build_wcrt(c))) return fail(rc);
     *out = c;
     return MFHE_OK;
@@ -419,8 +438,31 @@ extern "C" int mfhe_ctx_set_option(mfhe_ctx* c, int opt, int64_t v) {
             if (v < 0 || v > 2) return set_error(MFHE_EINVAL, "plan must be 0, 1 or 2");
             c->ntt_plan = (int)v;
             return MFHE_OK;
+        case MFHE_OPT_CRT_WORDS:
+            if (v < 1 || v > 32) return set_error(MFHE_EINVAL, "crt words must be in [1, 32]");
+            if (v <= c->W) return MFHE_OK;
+            return build_crt(c, (int)v);   // old tables stay in c->allocs until destroy
         default: return set_error(MFHE_EINVAL, "unknown option");
     }
+}
+
+extern "C" int mfhe_gl_perm_tables(const mfhe_ctx* c, const uint32_t** perm, const uint32_t** iperm) {
+    if (!c) return set_error(MFHE_EINVAL, "null ctx");
+    if (!(c->conv & MFHE_CONV_GL)) return set_error(MFHE_ENOTREADY, "no GL tables");
+    if (perm) *perm = c->gl_perm;
+    if (iperm) *iperm = c->gl_inv_perm;
+    return MFHE_OK;
+}
+
+extern "C" int mfhe_xy_tables(const mfhe_ctx* c, const double** V, const double** VT, const double** Vi,
+                              const double** ViT) {
+    if (!c) return set_error(MFHE_EINVAL, "null ctx");
+    if (int rc = ensure_xy(const_cast<mfhe_ctx*>(c))) return rc;   // lazily built tables, logically const
+    if (V) *V = (const double*)c->d_encV;
+    if (VT) *VT = (const double*)c->d_encVT;
+    if (Vi) *Vi = (const double*)c->d_encVi;
+    if (ViT) *ViT = (const double*)c->d_encViT;
+    return MFHE_OK;
 }
 
 extern "C" int mfhe_ctx_get_option(const mfhe_ctx* c, int opt, int64_t* v) {
@@ -428,6 +470,7 @@ extern "C" int mfhe_ctx_get_option(const mfhe_ctx* c, int opt, int64_t* v) {
     switch (opt) {
         case MFHE_OPT_NTT_CHUNK_BYTES: *v = c->ntt_chunk_bytes; return MFHE_OK;
         case MFHE_OPT_NTT_PLAN: *v = c->ntt_plan; return MFHE_OK;
+        case MFHE_OPT_CRT_WORDS: *v = c->W; return MFHE_OK;
         default: return set_error(MFHE_EINVAL, "unknown option");
     }
 }

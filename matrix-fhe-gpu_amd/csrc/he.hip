@@ -158,6 +158,63 @@ __global__ void center_limb0_kernel(const uint64_t* in, int64_t* out, uint64_t q
     out[i] = (a > (q >> 1)) ? (int64_t)a - (int64_t)q : (int64_t)a;
 }
 
+// (hi:lo) mod q: fold hi with r64 = 2^64 mod q, then one Barrett step (mu = floor(2^64 / q))
+__device__ __forceinline__ uint64_t mod128(unsigned __int128 v, uint64_t q, uint64_t mu, uint64_t r64) {
+    uint64_t hi = (uint64_t)(v >> 64), lo = (uint64_t)v;
+    while (hi) {
+        const unsigned __int128 t = (unsigned __int128)hi * r64 + lo;
+        hi = (uint64_t)(t >> 64);
+        lo = (uint64_t)t;
+    }
+    uint64_t r = lo - __umul64hi(lo, mu) * q;
+    return r >= q ? r - q : r;
+}
+
+// add_ct_kernel HE.cu:631-645 / mul_tensor_kernel HE.cu:648-669 over matrix-major [phi][L][n2]
+// (limb = (idx / n2) % L).  `half` = words of one ciphertext component.
+__global__ void ct_add_kernel(const uint64_t* x, const uint64_t* y, uint64_t* r,
+                              const uint64_t* qmu, int L, int log_n2, uint64_t half) {
+    const uint64_t idx = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x;
+    if (idx >= 2 * half) return;
+    const int l = (int)(((idx % half) >> log_n2) % (uint64_t)L);
+    const uint64_t q = qmu[2 * l];
+    const uint64_t s = x[idx] + y[idx];
+    r[idx] = s >= q ? s - q : s;
+}
+__global__ void ct_mul_kernel(const uint64_t* __restrict__ c1, const uint64_t* __restrict__ c2, uint64_t* d0,
+                              uint64_t* d1, uint64_t* d2, const uint64_t* qmu, const uint64_t* r64, int L, int log_n2,
+                              uint64_t half) {
+    const uint64_t idx = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x;
+    if (idx >= half) return;
+    const int l = (int)((idx >> log_n2) % (uint64_t)L);
+    const uint64_t q = qmu[2 * l], mu = qmu[2 * l + 1], rr = r64[l];
+    const uint64_t b1 = c1[idx], a1 = c1[half + idx], b2 = c2[idx], a2 = c2[half + idx];
+    using u128 = unsigned __int128;
+    d0[idx] = mod128((u128)b1 * b2, q, mu, rr);
+    const uint64_t t1 = mod128((u128)b1 * a2, q, mu, rr), t2 = mod128((u128)a1 * b2, q, mu, rr);
+    const uint64_t t = t1 + t2;
+    d1[idx] = t >= q ? t - q : t;
+    d2[idx] = mod128((u128)a1 * a2, q, mu, rr);
+}
+
+// planar <-> interleaved complex for the split re/im W-DFT entry points (HE.cu:472-502)
+__global__ void pack_i64_pair_kernel(const int64_t* re, const int64_t* im, double2* out, uint64_t total) {
+    const uint64_t i = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x;
+    if (i < total) out[i] = make_double2((double)re[i], (double)im[i]);
+}
+__global__ void pack_f64_pair_kernel(const double* re, const double* im, double2* out, uint64_t total) {
+    const uint64_t i = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x;
+    if (i < total) out[i] = make_double2(re[i], im[i]);
+}
+__global__ void unpack_pair_kernel(const double2* in, double* re, double* im, uint64_t total) {
+    const uint64_t i = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x;
+    if (i < total) {
+        const double2 v = in[i];
+        re[i] = v.x;
+        im[i] = v.y;
+    }
+}
+
 // ---------------- helpers ----------------
 static int need_wcrt(const mfhe_ctx* c) {
     if (!c) return set_error(MFHE_EINVAL, "null ctx");
@@ -277,6 +334,7 @@ static int layout(const mfhe_ctx* c, const uint64_t* in, uint64_t* out, bool to_
 static int encode_impl(mfhe_ctx* c, const double* msg, uint64_t* out_re, uint64_t* out_im, hipStream_t s) {
     RC(need_wcrt(c));
     if (!msg || !out_re || !out_im) return set_error(MFHE_EINVAL, "mfhe_encode: null pointer");
+    RC(ensure_xy(c));
     RC(ensure_ws(c));
     const Geo2 g = geo(c);
     Bump b{(char*)c->ws};
@@ -299,6 +357,7 @@ static int decode_impl(mfhe_ctx* c, const uint64_t* ev_re, const uint64_t* ev_im
                        Bump* pb = nullptr) {
     RC(need_wcrt(c));
     if (!ev_re || !ev_im || !msg) return set_error(MFHE_EINVAL, "mfhe_decode: null pointer");
+    RC(ensure_xy(c));
     Bump b0{(char*)c->ws};
     if (!pb) {
         RC(ensure_ws(c));
@@ -475,10 +534,11 @@ extern "C" int mfhe_wdft_inv(mfhe_ctx* c, const double* in, double* out, mfhe_st
 }
 
 static int xy_entry(mfhe_ctx* c, const double* in, double* out, size_t lanes, mfhe_stream_t s, bool inv) {
-    RC(need_wcrt(c));
+    if (!c) return set_error(MFHE_EINVAL, "null ctx");
     if (lanes == 0) return MFHE_OK;
     if (!in || !out || in == out) return set_error(MFHE_EINVAL, "mfhe_xy_(i)dft: need distinct in/out");
     if (lanes > 65535) return set_error(MFHE_EINVAL, "mfhe_xy_(i)dft: at most 65535 lanes per call");
+    RC(ensure_xy(c));
     RC(ensure_ws(c));
     double2* tmp = (double2*)c->ws;
     const Geo2 g = geo(c);
@@ -544,4 +604,54 @@ extern "C" int mfhe_decrypt_and_decode(mfhe_ctx* c, const uint64_t* cre, const u
     RC(decrypt_impl(c, cim, sk, ei, (hipStream_t)s, &inner));
     inner = b;
     return decode_impl(c, er, ei, msg, (hipStream_t)s, &inner);
+}
+
+static int wdft_pair(mfhe_ctx* c, const void* re, const void* im, bool i64, double* ore, double* oim, bool inv,
+                     hipStream_t s) {
+    RC(need_wcrt(c));
+    if (!re || !im || !ore || !oim) return set_error(MFHE_EINVAL, "mfhe_wdft_*_pair: null pointer");
+    RC(ensure_ws(c));
+    const Geo2 g = geo(c);
+    Bump b{(char*)c->ws};
+    double2* x = b.get<double2>(g.cnt);
+    double2* y = b.get<double2>(g.cnt);
+    if (i64)
+        hipLaunchKernelGGL(pack_i64_pair_kernel, g1(g.cnt), dim3(256), 0, s, (const int64_t*)re, (const int64_t*)im, x,
+                           g.cnt);
+    else
+        hipLaunchKernelGGL(pack_f64_pair_kernel, g1(g.cnt), dim3(256), 0, s, (const double*)re, (const double*)im, x,
+                           g.cnt);
+    MFHE_CHECK_LAUNCH("pack_pair_kernel");
+    RC(wdft(c, inv ? c->d_wdVinv : c->d_wdV, x, y, s));
+    hipLaunchKernelGGL(unpack_pair_kernel, g1(g.cnt), dim3(256), 0, s, y, ore, oim, g.cnt);
+    MFHE_CHECK_LAUNCH("unpack_pair_kernel");
+    return MFHE_OK;
+}
+extern "C" int mfhe_wdft_fwd_pair_i64(mfhe_ctx* c, const int64_t* re, const int64_t* im, double* ore, double* oim,
+                                      mfhe_stream_t s) {
+    return wdft_pair(c, re, im, true, ore, oim, false, (hipStream_t)s);
+}
+extern "C" int mfhe_wdft_inv_pair(mfhe_ctx* c, const double* re, const double* im, double* ore, double* oim,
+                                  mfhe_stream_t s) {
+    return wdft_pair(c, re, im, false, ore, oim, true, (hipStream_t)s);
+}
+
+extern "C" int mfhe_ct_add(mfhe_ctx* c, const uint64_t* x, const uint64_t* y, uint64_t* r, mfhe_stream_t s) {
+    if (!c) return set_error(MFHE_EINVAL, "null ctx");
+    if (!x || !y || !r) return set_error(MFHE_EINVAL, "mfhe_ct_add: null pointer");
+    const Geo2 g = geo(c);
+    hipLaunchKernelGGL(ct_add_kernel, g1(2 * g.words), dim3(256), 0, (hipStream_t)s, x, y, r, c->d_rns_mu, g.L,
+                       2 * g.logn, g.words);
+    MFHE_CHECK_LAUNCH("ct_add_kernel");
+    return MFHE_OK;
+}
+extern "C" int mfhe_ct_mul_tensor(mfhe_ctx* c, const uint64_t* x, const uint64_t* y, uint64_t* d0, uint64_t* d1,
+                                  uint64_t* d2, mfhe_stream_t s) {
+    if (!c) return set_error(MFHE_EINVAL, "null ctx");
+    if (!x || !y || !d0 || !d1 || !d2) return set_error(MFHE_EINVAL, "mfhe_ct_mul_tensor: null pointer");
+    const Geo2 g = geo(c);
+    hipLaunchKernelGGL(ct_mul_kernel, g1(g.words), dim3(256), 0, (hipStream_t)s, x, y, d0, d1, d2, c->d_rns_mu,
+                       c->d_r64, g.L, 2 * g.logn, g.words);
+    MFHE_CHECK_LAUNCH("ct_mul_kernel");
+    return MFHE_OK;
 }

@@ -19,6 +19,7 @@ namespace mfhe {
 // thread-local error reporting
 int set_error(int code, const std::string& msg);
 int hip_error(hipError_t e, const char* what);
+int ensure_xy(mfhe_ctx* c);   // XY encoder matrices, built on first use (ctx.cpp)
 
 #define MFHE_HIP(call)                                          \
     do {                                                        \

@@ -22,7 +22,7 @@ HEADER = REPO_ROOT / "include" / "mfhe.h"
 OK, EINVAL, EUNSUPPORTED, EHIP, ENOMEM, ENOTREADY = 0, 1, 2, 3, 4, 5
 CONV_PHANTOM, CONV_GL, CONV_WCRT = 1, 2, 4
 ARITH_AUTO, ARITH_F64, ARITH_U64 = 0, 1, 2
-OPT_NTT_CHUNK_BYTES, OPT_NTT_PLAN = 1, 2
+OPT_NTT_CHUNK_BYTES, OPT_NTT_PLAN, OPT_CRT_WORDS = 1, 2, 3
 
 #: reference parameters (include/core/config.h:7-52)
 RNS_MODULI = [
@@ -89,12 +89,17 @@ _sig("mfhe_rns_decompose", [_vp, _vp, _sz, _sz, _sz, _vp, _vp])
 _sig("mfhe_crt_compose", [_vp, _vp, _sz, _sz, _vp, _vp, _vp])
 _sig("mfhe_crt_to_f64", [_vp, _vp, _vp, _sz, _vp, _sz, _vp])
 _sig("mfhe_crt_compose_f64", [_vp, _vp, _sz, _sz, _vp, _sz, _vp])
+_sig("mfhe_crt_compose_f64_sharded", [_vp, _vp, ctypes.c_int, _sz, _sz, _sz, _vp, _sz, _vp])
 for _n in ("mfhe_wcrt_fwd", "mfhe_wcrt_inv", "mfhe_wcrt_fwd_vector", "mfhe_wcrt_fwd_centered",
            "mfhe_wcrt_inv_centered", "mfhe_wdft_fwd", "mfhe_wdft_inv", "mfhe_matrix_to_poly", "mfhe_poly_to_matrix",
            "mfhe_keygen"):
     _sig(_n, [_vp, _vp, _vp, _vp] if _n != "mfhe_keygen" else [_vp, _vp, _vp])
 _sig("mfhe_xy_idft", [_vp, _vp, _vp, _sz, _vp])
 _sig("mfhe_xy_dft", [_vp, _vp, _vp, _sz, _vp])
+_sig("mfhe_wdft_fwd_pair_i64", [_vp] * 6)
+_sig("mfhe_wdft_inv_pair", [_vp] * 6)
+_sig("mfhe_ct_add", [_vp] * 5)
+_sig("mfhe_ct_mul_tensor", [_vp] * 7)
 _sig("mfhe_ctx_reserve_workspace", [_vp])
 _sig("mfhe_encode", [_vp, _vp, _vp, _vp, _vp])
 _sig("mfhe_decode", [_vp, _vp, _vp, _vp, _vp])
@@ -248,6 +253,14 @@ class Context:
         return out
 
 
+    def crt_compose_f64_sharded(self, src, out, nshards, shard_stride, npoly, ncoeff, out_stride=1, stream=None,
+                                src_offset=0):
+        """Compose residue shards gathered from `nshards` GPUs in place (see include/mfhe.h)."""
+        check(lib.mfhe_crt_compose_f64_sharded(self._h, _ptr(src) + 8 * src_offset, nshards, shard_stride, npoly,
+                                               ncoeff, _ptr(out), out_stride, _stream_ptr(stream)),
+              "crt_compose_f64_sharded")
+        return out
+
     # ---- W axis / encoder / pipelines (reference geometry, CONV_WCRT) ----
     def _call(self, name, *ptrs, stream=None):
         fn = getattr(lib, name)
@@ -263,6 +276,14 @@ class Context:
         self._call("mfhe_wcrt_inv_centered", _ptr(src), _ptr(dst), stream=stream); return dst
     def wdft_fwd(self, src, dst, stream=None): self._call("mfhe_wdft_fwd", _ptr(src), _ptr(dst), stream=stream); return dst
     def wdft_inv(self, src, dst, stream=None): self._call("mfhe_wdft_inv", _ptr(src), _ptr(dst), stream=stream); return dst
+    def wdft_fwd_pair_i64(self, re, im, out_re, out_im, stream=None):
+        self._call("mfhe_wdft_fwd_pair_i64", _ptr(re), _ptr(im), _ptr(out_re), _ptr(out_im), stream=stream)
+    def wdft_inv_pair(self, re, im, out_re, out_im, stream=None):
+        self._call("mfhe_wdft_inv_pair", _ptr(re), _ptr(im), _ptr(out_re), _ptr(out_im), stream=stream)
+    def ct_add(self, ct1, ct2, res, stream=None):
+        self._call("mfhe_ct_add", _ptr(ct1), _ptr(ct2), _ptr(res), stream=stream); return res
+    def ct_mul_tensor(self, ct1, ct2, d0, d1, d2, stream=None):
+        self._call("mfhe_ct_mul_tensor", _ptr(ct1), _ptr(ct2), _ptr(d0), _ptr(d1), _ptr(d2), stream=stream)
     def xy_dft(self, src, dst, lanes, stream=None):
         check(lib.mfhe_xy_dft(self._h, _ptr(src), _ptr(dst), lanes, _stream_ptr(stream)), "xy_dft"); return dst
     def xy_idft(self, src, dst, lanes, stream=None):

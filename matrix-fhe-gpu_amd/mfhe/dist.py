@@ -1,0 +1,69 @@
+"""Multi-GPU residue sharding: RCCL exchange + in-place sharded CRT recombine.
+
+Layout: with `world` ranks and L limbs, rank g owns limbs [g*Lg, (g+1)*Lg), Lg = L / world, for every
+polynomial of the batch: a [batch][Lg][ncoeff] u64 shard (NTT, RNS decompose and W-CRT are
+per-limb and need no communication).  Wide CRT recombine needs all L residues of a coefficient,
+so it is the one exchange step.  Rank g recombines the batch slice [g*B/world, (g+1)*B/world):
+
+  allgather : all_gather_into_tensor -> [world][batch][Lg][n]; every rank receives (world-1)/world
+              of the whole residue set and composes its slice in place.
+  alltoall  : all_to_all_single       -> [world][batch/world][Lg][n]; every rank receives only the
+              missing limbs of its own slice ((world-1)/world^2 of the residue set).
+
+Both hand the received buffer to mfhe_crt_compose_f64_sharded, which reads the shards in place
+(no transpose).  On GPU the process group is RCCL (backend "nccl"); the CPU tests drive the same
+exchange over gloo.
+"""
+from __future__ import annotations
+
+import torch
+import torch.distributed as dist
+
+
+def limb_range(L: int, world: int, rank: int) -> tuple[int, int]:
+    """(start_limb, nlimbs) owned by `rank` under residue sharding."""
+    if L % world:
+        raise ValueError(f"L={L} must be a multiple of world={world}")
+    lg = L // world
+    return rank * lg, lg
+
+
+def exchange_residues(shard: torch.Tensor, batch: int, lg: int, ncoeff: int, mode: str = "allgather", group=None):
+    """Exchange this rank's [batch][lg][ncoeff] residue shard.
+
+    Returns (buf, offset, shard_stride, npoly): this rank's batch slice is `world` shards starting at
+    word `offset` of `buf`, `shard_stride` words apart, each [npoly][lg][ncoeff].
+    """
+    world = dist.get_world_size(group)
+    rank = dist.get_rank(group)
+    if shard.numel() != batch * lg * ncoeff:
+        raise ValueError("shard size does not match batch * lg * ncoeff")
+    if batch % world:
+        raise ValueError(f"batch={batch} must be a multiple of world={world}")
+    bs = batch // world
+    shard = shard.reshape(-1)
+    if mode == "allgather":
+        buf = torch.empty(world * shard.numel(), dtype=shard.dtype, device=shard.device)
+        dist.all_gather_into_tensor(buf, shard, group=group)
+        return buf, rank * bs * lg * ncoeff, batch * lg * ncoeff, bs
+    if mode == "alltoall":
+        buf = torch.empty(world * bs * lg * ncoeff, dtype=shard.dtype, device=shard.device)
+        dist.all_to_all_single(buf, shard, group=group)   # chunk r of the input = polys of rank r's slice
+        return buf, 0, bs * lg * ncoeff, bs
+    raise ValueError(f"unknown exchange mode {mode!r}")
+
+
+def crt_recombine(ctx, shard: torch.Tensor, batch: int, ncoeff: int, mode: str = "allgather", group=None,
+                  out: torch.Tensor | None = None, stream=None) -> torch.Tensor:
+    """Exchange residue shards and compose this rank's batch slice to f64 (centred value / delta).
+
+    `ctx` is an mfhe.Context over all L moduli (its CRT tables); returns [batch/world][ncoeff] f64.
+    """
+    world = dist.get_world_size(group)
+    L = ctx.info().num_limbs
+    _, lg = limb_range(L, world, 0)
+    buf, off, stride, bs = exchange_residues(shard, batch, lg, ncoeff, mode, group)
+    if out is None:
+        out = torch.empty(bs * ncoeff, dtype=torch.float64, device=shard.device)
+    ctx.crt_compose_f64_sharded(buf, out, world, stride, bs, ncoeff, stream=stream, src_offset=off)
+    return out

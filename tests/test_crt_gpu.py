@@ -103,3 +103,31 @@ def test_decompose_compose_roundtrip_full_size(mfhe):
     expect = torch.trunc(zd + torch.copysign(torch.full_like(zd, 0.5), zd)) / ctx.delta   # llround: ties away
     assert (torch.round(zd) != torch.trunc(zd + torch.copysign(torch.full_like(zd, 0.5), zd))).any()
     assert torch.equal(out, expect)
+
+
+@pytest.mark.parametrize("world", [2, 4, 8])
+def test_crt_compose_f64_sharded_matches_unsharded(mfhe, orc, world):
+    """mfhe_crt_compose_f64_sharded reads the all-gather / all-to-all receive layouts in place."""
+    import torch
+    moduli = orc.gen_primes(50, 1 << 18, 16)
+    ctx = mfhe.Context(moduli, 16, mfhe.CONV_PHANTOM)
+    B, L, N = 2 * world, 16, 2048
+    lg, bs = L // world, 2
+    rng = np.random.default_rng(world)
+    full = rng.integers(0, 2 ** 63, (B, L, N), dtype=np.uint64) % np.array(moduli, np.uint64)[None, :, None]
+    ref = torch.empty(bs * N, dtype=torch.float64, device="cuda")
+    got = torch.empty_like(ref)
+    # all-gather layout: [world][B][lg][N]; rank r composes polys [r*bs, (r+1)*bs)
+    gathered = np.concatenate([full[:, g * lg:(g + 1) * lg, :].ravel() for g in range(world)])
+    dg = mfhe.to_device_u64(gathered)
+    # all-to-all layout for rank r: [world][bs][lg][N]
+    for r in (0, world - 1):
+        mine = mfhe.to_device_u64(full[r * bs:(r + 1) * bs].ravel())
+        ctx.crt_compose_f64(mine, ref, bs, N)
+        ctx.crt_compose_f64_sharded(dg, got, world, B * lg * N, bs, N, src_offset=r * bs * lg * N)
+        torch.cuda.synchronize()
+        assert torch.equal(got, ref)
+        a2a = np.concatenate([full[r * bs:(r + 1) * bs, g * lg:(g + 1) * lg, :].ravel() for g in range(world)])
+        ctx.crt_compose_f64_sharded(mfhe.to_device_u64(a2a), got, world, bs * lg * N, bs, N)
+        torch.cuda.synchronize()
+        assert torch.equal(got, ref)

@@ -152,6 +152,60 @@ def test_wdft_and_xy_transforms_vs_oracle(mfhe, orc, small):
     assert np.max(np.abs(mt2.cpu().numpy().view(np.complex128) - M)) < 1e-10
 
 
+def test_wdft_pair_entry_points(mfhe, orc, small):
+    """wdft_forward_centered_pair / wdft_inverse_pair (HE.cu:472-502, 1116-1145, 1174-1202): planar re/im."""
+    import torch
+    n, ctx, h = small
+    n2 = n * n
+    rng = np.random.default_rng(5)
+    re = rng.integers(-2 ** 40, 2 ** 40, 512 * n2, dtype=np.int64)
+    im = rng.integers(-2 ** 40, 2 ** 40, 512 * n2, dtype=np.int64)
+    V = np.zeros(512 * 512 * 2)
+    Vi = np.zeros(512 * 512 * 2)
+    assert orc.L.orc_wdft_tables(P(V), P(Vi)) == 0
+    z = (re.astype(np.float64) + 1j * im.astype(np.float64)).astype(np.complex128)
+    ref = np.zeros(512 * n2 * 2)
+    orc.L.orc_wdft_forward(P(np.ascontiguousarray(z.view(np.float64))), P(ref), P(V), n2, 512)
+    ref = ref.view(np.complex128)
+    ore = torch.empty(512 * n2, dtype=torch.float64, device="cuda")
+    oim = torch.empty_like(ore)
+    ctx.wdft_fwd_pair_i64(torch.from_numpy(re).cuda(), torch.from_numpy(im).cuda(), ore, oim)
+    torch.cuda.synchronize()
+    scale = np.max(np.abs(ref))
+    assert np.max(np.abs(ore.cpu().numpy() - ref.real)) <= FP_TOL * scale
+    assert np.max(np.abs(oim.cpu().numpy() - ref.imag)) <= FP_TOL * scale
+    bre = torch.empty_like(ore)
+    bim = torch.empty_like(ore)
+    ctx.wdft_inv_pair(ore, oim, bre, bim)
+    torch.cuda.synchronize()
+    assert np.max(np.abs(bre.cpu().numpy() - re)) < 1e-9 * 2 ** 40
+    assert np.max(np.abs(bim.cpu().numpy() - im)) < 1e-9 * 2 ** 40
+
+
+def test_ct_add_and_mul_tensor_bit_exact(mfhe, small):
+    """add_ciphertexts / multiply_ciphertexts_raw (HE.cu:631-669, 1710-1740) on matrix-major [b | a]."""
+    import torch
+    n, ctx, h = small
+    rng = np.random.default_rng(6)
+    c1 = np.concatenate([_rand_mat(rng, n), _rand_mat(rng, n)])
+    c2 = np.concatenate([_rand_mat(rng, n), _rand_mat(rng, n)])
+    half = c1.size // 2
+    q = np.broadcast_to(np.array(RNS, np.uint64)[None, :, None], (512, 11, n * n)).ravel()
+    res = torch.empty(c1.size, dtype=torch.int64, device="cuda")
+    ctx.ct_add(_dev(mfhe, c1), _dev(mfhe, c2), res)
+    qq = np.concatenate([q, q])
+    s = c1 + c2
+    np.testing.assert_array_equal(mfhe.to_host_u64(res), np.where(s >= qq, s - qq, s))
+    d = [torch.empty(half, dtype=torch.int64, device="cuda") for _ in range(3)]
+    ctx.ct_mul_tensor(_dev(mfhe, c1), _dev(mfhe, c2), *d)
+    torch.cuda.synchronize()
+    O = lambda a: a.astype(object)
+    b1, a1, b2, a2, qo = O(c1[:half]), O(c1[half:]), O(c2[:half]), O(c2[half:]), O(q)
+    want = [(b1 * b2) % qo, (b1 * a2 + a1 * b2) % qo, (a1 * a2) % qo]
+    for got, w in zip(d, want):
+        np.testing.assert_array_equal(mfhe.to_host_u64(got), w.astype(np.uint64))
+
+
 def test_keygen_bit_exact_reference_geometry(mfhe, orc):
     """generate_secret_key (HE.cu:1272-1307): ternary s -> W-CRT -> X-NTT; no floating point -> exact."""
     import torch

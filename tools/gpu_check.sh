@@ -11,7 +11,7 @@ OUT=$ROOT/gpurun_out/$TAG
 mkdir -p "$OUT"
 cd "$ROOT"
 
-timeout -k 10 900 python -m pytest $SEL -m gpu -q -rf > "$OUT/pytest_gpu.log" 2>&1
+timeout -k 10 900 python -u -m pytest $SEL -m gpu -v -rf --timeout 400 --durations 15 > "$OUT/pytest_gpu.log" 2>&1
 rc=$?
 tail -25 "$OUT/pytest_gpu.log"
 if [ $rc -ne 0 ] && [ $rc -ne 1 ] && [ $rc -ne 5 ]; then echo "pytest crashed rc=$rc"; exit $rc; fi
