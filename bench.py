@@ -36,6 +36,9 @@ def parse():
     ap.add_argument("--limbs", type=int, default=8)
     ap.add_argument("--batch", type=int, default=1024)
     ap.add_argument("--arith", type=int, default=0, help="0 auto, 1 f64, 2 u64")
+    ap.add_argument("--ntt-wg", type=int, default=None, help="MFHE_OPT_NTT_WG_PER_CU override (tuning)")
+    ap.add_argument("--ntt-prefetch", type=int, default=None, help="MFHE_OPT_NTT_PREFETCH override (tuning)")
+    ap.add_argument("--ntt-chunk", type=int, default=None, help="MFHE_OPT_NTT_CHUNK_BYTES override (tuning)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-seconds", type=float, default=10.0)
     ap.add_argument("--only", default="all", help="all | ntt | crt | recombine (profiling)")
@@ -126,6 +129,9 @@ def main():
     ctx = mfhe.Context(moduli, log_n, mfhe.CONV_PHANTOM)
     if args.arith:
         ctx.set_arith(args.arith)
+    for opt, val in ((4, args.ntt_wg), (5, args.ntt_prefetch), (mfhe.OPT_NTT_CHUNK_BYTES, args.ntt_chunk)):
+        if val is not None:
+            ctx.set_option(opt, val)
     stream = torch.cuda.current_stream()
 
     # synthetic residues uniform in [0, q_l), generated on device

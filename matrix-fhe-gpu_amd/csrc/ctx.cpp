@@ -306,6 +306,8 @@ static int ctx_create_impl(const uint64_t* moduli, int L, int logN, int conv, do
     hipError_t he = hipGetDevice(&c->device);
     int rc = MFHE_OK;
     if (he != hipSuccess) rc = hip_error(he, "hipGetDevice");
+    if (!rc && (he = hipDeviceGetAttribute(&c->num_cus, hipDeviceAttributeMultiprocessorCount, c->device)) != hipSuccess)
+        rc = hip_error(he, "hipDeviceGetAttribute");
 
     auto fail = [&](int code) {
         for (void* p : c->allocs) (void)hipFree(p);
@@ -438,6 +440,14 @@ extern "C" int mfhe_ctx_set_option(mfhe_ctx* c, int opt, int64_t v) {
             if (v < 0 || v > 2) return set_error(MFHE_EINVAL, "plan must be 0, 1 or 2");
             c->ntt_plan = (int)v;
             return MFHE_OK;
+        case MFHE_OPT_NTT_WG_PER_CU:
+            if (v < 0 || v > 16) return set_error(MFHE_EINVAL, "workgroups per CU must be in [0, 16]");
+            c->ntt_wg_per_cu = (int)v;
+            return MFHE_OK;
+        case MFHE_OPT_NTT_PREFETCH:
+            if (v < 0 || v > 1) return set_error(MFHE_EINVAL, "prefetch must be 0 or 1");
+            c->ntt_prefetch = (int)v;
+            return MFHE_OK;
         case MFHE_OPT_CRT_WORDS:
             if (v < 1 || v > 32) return set_error(MFHE_EINVAL, "crt words must be in [1, 32]");
             if (v <= c->W) return MFHE_OK;
@@ -470,6 +480,8 @@ extern "C" int mfhe_ctx_get_option(const mfhe_ctx* c, int opt, int64_t* v) {
     switch (opt) {
         case MFHE_OPT_NTT_CHUNK_BYTES: *v = c->ntt_chunk_bytes; return MFHE_OK;
         case MFHE_OPT_NTT_PLAN: *v = c->ntt_plan; return MFHE_OK;
+        case MFHE_OPT_NTT_WG_PER_CU: *v = c->ntt_wg_per_cu; return MFHE_OK;
+        case MFHE_OPT_NTT_PREFETCH: *v = c->ntt_prefetch; return MFHE_OK;
         case MFHE_OPT_CRT_WORDS: *v = c->W; return MFHE_OK;
         default: return set_error(MFHE_EINVAL, "unknown option");
     }

@@ -86,26 +86,24 @@ __device__ __forceinline__ void static_for(F&& f) {
     }
 }
 
-template <class A, class TS, int LOG_G, int LOG_R, int NG, bool COLS, bool INV, bool IN_RAW, bool OUT_RAW,
-          bool TWIST, bool BREV>
-__global__ __launch_bounds__(NG * (1 << (LOG_G - LOG_R))) void ntt_pass_kernel(PassArgs<TS> a) {
-    using Gm = Geo<LOG_G, LOG_R>;
-    using T = typename A::T;
-    using Tw = typename A::Tw;
-    constexpr int R = Gm::R, TG = Gm::TG, NR = Gm::NR, GS = Gm::GS;
-    extern __shared__ __attribute__((aligned(16))) uint64_t lds[];
+// Where one tile (NG groups) of a pass lives: limb/batch, base pointer, twiddle offset, (hi, lo).
+// UNI: every group of the tile lies in one polynomial (two-pass plans; single pass with NG = 1), so the
+// base pointer is workgroup-uniform and each element address is an SGPR base + 32-bit lane offset.
+struct TileLoc {
+    uint64_t* base;
+    size_t twoff;
+    uint32_t off0;    // jhi | lo  (element offset inside the polynomial, without the group index)
+    uint64_t hi;
+    int mod;
+    bool active;
+};
 
-    const uint32_t t = threadIdx.x;
-    const uint32_t gl = COLS ? (t % NG) : (t / TG);
-    const uint32_t tau = COLS ? (t / NG) : (t % TG);
-
-    const int logN = a.logN;
-    const int logS = logN - a.s0 - LOG_G;
-    const uint64_t S = 1ull << logS;
-    const int log_gpp = logS + a.s0;  // log2(groups per polynomial-limb)
-    const uint32_t npl = (uint32_t)(a.batch * (uint64_t)a.nl);   // launcher guarantees < 2^32
-    const uint32_t lb = xcd_remap(blockIdx.x, a.nblocks);
-
+template <int LOG_G, int NG, bool COLS, bool UNI>
+__device__ __forceinline__ TileLoc tile_loc(uint64_t* data, uint64_t batch, int nl, int start_limb, int logN, int s0,
+                                            uint32_t lb, uint32_t gl) {
+    const int logS = logN - s0 - LOG_G;
+    const int log_gpp = logS + s0;  // log2(groups per polynomial-limb)
+    const uint32_t npl = (uint32_t)(batch * (uint64_t)nl);   // launcher guarantees < 2^32
     uint32_t v;
     uint64_t hi, lo;
     if constexpr (COLS) {
@@ -116,141 +114,227 @@ __global__ __launch_bounds__(NG * (1 << (LOG_G - LOG_R))) void ntt_pass_kernel(P
         const uint32_t tile = lb & ((1u << log_tpp) - 1);
         hi = tile >> log_ct;
         lo = ((uint64_t)(tile & ((1u << log_ct) - 1)) << LOG_NG) + gl;
+    } else if constexpr (UNI) {
+        const uint64_t g0 = (uint64_t)lb * NG;   // NG divides groups-per-poly: v is workgroup-uniform
+        v = (uint32_t)(g0 >> log_gpp);
+        const uint64_t rem = (g0 & ((1ull << log_gpp) - 1)) + gl;
+        hi = rem >> logS;
+        lo = rem & ((1ull << logS) - 1);
     } else {
         const uint64_t gid = (uint64_t)lb * NG + gl;
         v = (uint32_t)(gid >> log_gpp);
         const uint64_t rem = gid & ((1ull << log_gpp) - 1);
         hi = rem >> logS;
-        lo = rem & (S - 1);
+        lo = rem & ((1ull << logS) - 1);
     }
-    const bool active = v < npl;
-    if (!active) v = 0;
+    TileLoc t;
+    t.active = v < npl;
+    if (!t.active) v = 0;   // inactive tail lanes read a valid polynomial and store nothing
     // virtual poly index is limb-major: v = l * batch + b
-    const uint32_t bt = (uint32_t)a.batch;
+    const uint32_t bt = (uint32_t)batch;
     const int l = (int)(v / bt);
     const uint64_t b = v - (uint32_t)l * bt;
-    const int mod = a.start_limb + l;
-    const uint64_t N = 1ull << logN;
-    uint64_t* base = a.data + (b * (uint64_t)a.nl + (uint64_t)l) * N;
-    const size_t twoff = (size_t)mod * N;
-    LimbConst lc;
-    if (a.limbs) {
-        lc = a.limbs[mod];
-    } else {
-        lc.q = a.qraw[(size_t)mod * a.qstride];
-        lc.qf = (double)lc.q;
-        lc.qinv = 1.0 / lc.qf;
+    t.mod = start_limb + l;
+    t.base = data + ((b * (uint64_t)nl + (uint64_t)l) << logN);
+    t.twoff = (size_t)t.mod << logN;
+    t.hi = hi;
+    t.off0 = (uint32_t)((hi << (logN - s0)) | lo);
+    return t;
+}
+
+// One pass of the transform: LOG_G stages on groups of G = 2^LOG_G elements, one tile (NG groups) per
+// workgroup at a time.  Split into locate / load / compute+store so the persistent pass kernel can
+// prefetch and the fused kernel can run two different passes in one launch.
+template <class A, class TS, int LOG_G, int LOG_R, int NG, bool COLS, bool INV, bool IN_RAW, bool OUT_RAW,
+          bool TWIST, bool BREV, bool UNI>
+struct NttPass {
+    using Gm = Geo<LOG_G, LOG_R>;
+    using T = typename A::T;
+    using Tw = typename A::Tw;
+    static constexpr int R = Gm::R, TG = Gm::TG, NR = Gm::NR, GS = Gm::GS;
+    static constexpr int NT = NG * TG;
+    static constexpr size_t LDS_BYTES = (NR > 1 || BREV) ? (size_t)NG * GS * sizeof(uint64_t) : 0;
+    static constexpr int r_load = (INV && COLS) ? (NR - 1) : 0;
+    static constexpr int r_store = (!INV && COLS) ? (NR - 1) : 0;
+
+    const PassArgs<TS>& a;
+    uint32_t gl, tau;
+    int logS;
+
+    __device__ __forceinline__ explicit NttPass(const PassArgs<TS>& args) : a(args) {
+        const uint32_t t = threadIdx.x;
+        gl = COLS ? (t % NG) : (t / TG);
+        tau = COLS ? (t / NG) : (t % TG);
+        logS = a.logN - a.s0 - LOG_G;
     }
-    const A ar(lc);
+    __device__ __forceinline__ uint32_t jidx(const TileLoc& L, uint32_t g) const { return L.off0 | (g << logS); }
+    __device__ __forceinline__ TileLoc locate(uint32_t lb) const {
+        return tile_loc<LOG_G, NG, COLS, UNI>(a.data, a.batch, a.nl, a.start_limb, a.logN, a.s0, lb, gl);
+    }
+    __device__ __forceinline__ void load(const TileLoc& L, uint64_t (&raw)[R]) const {
+#pragma unroll
+        for (int k = 0; k < R; ++k) raw[k] = L.base[jidx(L, Gm::g_of(r_load, tau, k))];
+    }
 
-    const uint64_t jhi = hi << (logN - a.s0);
-    auto jidx = [&](uint32_t g) -> uint64_t { return jhi | ((uint64_t)g << logS) | lo; };
+    __device__ __forceinline__ void compute_store(const TileLoc& L, const uint64_t (&raw)[R], uint64_t* lds) const {
+        uint64_t* my_lds = lds + (size_t)gl * GS;
+        LimbConst lc;
+        if (a.limbs) {
+            lc = a.limbs[L.mod];
+        } else {
+            lc.q = a.qraw[(size_t)L.mod * a.qstride];
+            lc.qf = (double)lc.q;
+            lc.qinv = 1.0 / lc.qf;
+        }
+        const A ar(lc);
+        const size_t twoff = L.twoff;
+        const uint32_t tau_ = tau;
 
-    T x[R];
-    uint64_t* my_lds = lds + (size_t)gl * GS;
-
-    auto exchange = [&](auto rf, auto rt, bool brev_pos) {
-        constexpr int r_from = decltype(rf)::value, r_to = decltype(rt)::value;
-        __syncthreads();
+        T x[R];
 #pragma unroll
         for (int k = 0; k < R; ++k) {
-            uint32_t g = Gm::g_of(r_from, tau, k);
-            if (brev_pos) g = brev_bits(g, LOG_G);
-            my_lds[Gm::pad(g)] = A::to_raw(x[k]);
+            x[k] = IN_RAW ? A::from_raw(raw[k]) : A::from_u64(raw[k]);
+            if constexpr (TWIST && !INV) x[k] = ar.mulmod(x[k], a.twist.get(twoff + jidx(L, Gm::g_of(r_load, tau_, k))));
         }
-        __syncthreads();
-#pragma unroll
-        for (int k = 0; k < R; ++k) x[k] = A::from_raw(my_lds[Gm::pad(Gm::g_of(r_to, tau, k))]);
-    };
 
-    // ---- load ----
-    constexpr int r_load = (INV && COLS) ? (NR - 1) : 0;
+        auto exchange = [&](auto rf, auto rt, bool brev_pos) {
+            constexpr int r_from = decltype(rf)::value, r_to = decltype(rt)::value;
+            __syncthreads();
 #pragma unroll
-    for (int k = 0; k < R; ++k) {
-        const uint32_t g = Gm::g_of(r_load, tau, k);
-        // unconditional: inactive tail threads point at a valid polynomial (v = 0); a per-element
-        // "active ? load : 0" makes hipcc branch around every load with a vmcnt(0) each.
-        const uint64_t raw = base[jidx(g)];
-        x[k] = IN_RAW ? A::from_raw(raw) : A::from_u64(raw);
-        if constexpr (TWIST && !INV) x[k] = ar.mulmod(x[k], a.twist.get(twoff + jidx(g)));
-    }
-    if constexpr (INV && !COLS && (NR > 1 || BREV))
-        exchange(std::integral_constant<int, 0>{}, std::integral_constant<int, NR - 1>{}, BREV);
+            for (int k = 0; k < R; ++k) {
+                uint32_t g = Gm::g_of(r_from, tau_, k);
+                if (brev_pos) g = brev_bits(g, LOG_G);
+                my_lds[Gm::pad(g)] = A::to_raw(x[k]);
+            }
+            __syncthreads();
+#pragma unroll
+            for (int k = 0; k < R; ++k) x[k] = A::from_raw(my_lds[Gm::pad(Gm::g_of(r_to, tau_, k))]);
+        };
 
-    // ---- one stage on register bit bb of round r ----
-    auto stage = [&](auto rc, auto bc) {
-        constexpr int r = decltype(rc)::value, bb = decltype(bc)::value;
-        constexpr int hb = Gm::HB(r), wl = Gm::WL(r);
-        constexpr int bit = wl + bb;
-        if constexpr (bit <= hb) {
-            const int s = a.s0 + (LOG_G - 1 - bit);
-            constexpr int half = 1 << bb;
-            const uint64_t tau_hi = tau >> wl;
-            const uint64_t twb = twoff + (1ull << s) + (hi << (LOG_G - 1 - bit)) + (tau_hi << (LOG_R - 1 - bb));
-            if constexpr (!INV) {
-#pragma unroll
-                for (int k = 0; k < R; ++k) {
-                    if (k & half) continue;
-                    const Tw w = a.tw.get(twb + (uint64_t)(k >> (bb + 1)));
-                    ar.ct(x[k], x[k + half], w);
-                }
-            } else {
-                if (s == 0) {
-                    const Tw wn = a.ninv.get((size_t)mod);
-                    const Tw w1 = a.tw.get(twoff + 1);
-#pragma unroll
-                    for (int k = 0; k < R; ++k) {
-                        if (k & half) continue;
-                        T u = x[k], vv = x[k + half];
-                        ar.gs(u, vv, w1);          // u = red(u+v), vv = (u-v) * itw[1]
-                        x[k] = ar.mulmod(u, wn);   // X * n^-1
-                        x[k + half] = vv;
-                    }
-                } else {
+        if constexpr (INV && !COLS && (NR > 1 || BREV))
+            exchange(std::integral_constant<int, 0>{}, std::integral_constant<int, NR - 1>{}, BREV);
+
+        // ---- one stage on register bit bb of round r ----
+        auto stage = [&](auto rc, auto bc) {
+            constexpr int r = decltype(rc)::value, bb = decltype(bc)::value;
+            constexpr int hb = Gm::HB(r), wl = Gm::WL(r);
+            constexpr int bit = wl + bb;
+            if constexpr (bit <= hb) {
+                const int s = a.s0 + (LOG_G - 1 - bit);
+                constexpr int half = 1 << bb;
+                const uint64_t tau_hi = tau_ >> wl;
+                const uint64_t twb =
+                    twoff + (1ull << s) + (L.hi << (LOG_G - 1 - bit)) + (tau_hi << (LOG_R - 1 - bb));
+                if constexpr (!INV) {
 #pragma unroll
                     for (int k = 0; k < R; ++k) {
                         if (k & half) continue;
                         const Tw w = a.tw.get(twb + (uint64_t)(k >> (bb + 1)));
-                        ar.gs(x[k], x[k + half], w);
+                        ar.ct(x[k], x[k + half], w);
+                    }
+                } else {
+                    if (s == 0) {
+                        const Tw wn = a.ninv.get((size_t)L.mod);
+                        const Tw w1 = a.tw.get(twoff + 1);
+#pragma unroll
+                        for (int k = 0; k < R; ++k) {
+                            if (k & half) continue;
+                            T u = x[k], vv = x[k + half];
+                            ar.gs(u, vv, w1);          // u = red(u+v), vv = (u-v) * itw[1]
+                            x[k] = ar.mulmod(u, wn);   // X * n^-1
+                            x[k + half] = vv;
+                        }
+                    } else {
+#pragma unroll
+                        for (int k = 0; k < R; ++k) {
+                            if (k & half) continue;
+                            const Tw w = a.tw.get(twb + (uint64_t)(k >> (bb + 1)));
+                            ar.gs(x[k], x[k + half], w);
+                        }
                     }
                 }
             }
-        }
-    };
+        };
 
-    if constexpr (!INV) {
-        static_for<0, NR>([&](auto rc) {
-            constexpr int r = decltype(rc)::value;
-            if constexpr (r > 0) {
-                exchange(std::integral_constant<int, r - 1>{}, rc, false);
+        if constexpr (!INV) {
+            static_for<0, NR>([&](auto rc) {
+                constexpr int r = decltype(rc)::value;
+                if constexpr (r > 0) {
+                    exchange(std::integral_constant<int, r - 1>{}, rc, false);
 #pragma unroll
-                for (int k = 0; k < R; ++k) x[k] = ar.round_reduce(x[k]);
-            }
-            static_for<0, LOG_R>([&](auto bi) {
-                stage(rc, std::integral_constant<int, LOG_R - 1 - decltype(bi)::value>{});
+                    for (int k = 0; k < R; ++k) x[k] = ar.round_reduce(x[k]);
+                }
+                static_for<0, LOG_R>([&](auto bi) {
+                    stage(rc, std::integral_constant<int, LOG_R - 1 - decltype(bi)::value>{});
+                });
             });
-        });
-    } else {
-        static_for<0, NR>([&](auto ri) {
-            constexpr int r = NR - 1 - decltype(ri)::value;
-            if constexpr (r < NR - 1) exchange(std::integral_constant<int, r + 1>{}, std::integral_constant<int, r>{}, false);
-            static_for<0, LOG_R>([&](auto bi) { stage(std::integral_constant<int, r>{}, bi); });
-        });
-    }
+        } else {
+            static_for<0, NR>([&](auto ri) {
+                constexpr int r = NR - 1 - decltype(ri)::value;
+                if constexpr (r < NR - 1)
+                    exchange(std::integral_constant<int, r + 1>{}, std::integral_constant<int, r>{}, false);
+                static_for<0, LOG_R>([&](auto bi) { stage(std::integral_constant<int, r>{}, bi); });
+            });
+        }
 
-    // ---- store ----
-    constexpr int r_store = (!INV && COLS) ? (NR - 1) : 0;
-    if constexpr (!INV && !COLS && (NR > 1 || BREV))
-        exchange(std::integral_constant<int, NR - 1>{}, std::integral_constant<int, 0>{}, BREV);
-    if (active) {
+        // ---- store ----
+        if constexpr (!INV && !COLS && (NR > 1 || BREV))
+            exchange(std::integral_constant<int, NR - 1>{}, std::integral_constant<int, 0>{}, BREV);
+        if (L.active) {
 #pragma unroll
-        for (int k = 0; k < R; ++k) {
-            const uint32_t g = Gm::g_of(r_store, tau, k);
-            T y = x[k];
-            if constexpr (TWIST && INV) y = ar.mulmod(y, a.twist.get(twoff + jidx(g)));
-            base[jidx(g)] = OUT_RAW ? A::to_raw(ar.reduce(y)) : ar.canon(y);
+            for (int k = 0; k < R; ++k) {
+                const uint32_t g = Gm::g_of(r_store, tau_, k);
+                T y = x[k];
+                if constexpr (TWIST && INV) y = ar.mulmod(y, a.twist.get(twoff + jidx(L, g)));
+                L.base[jidx(L, g)] = OUT_RAW ? A::to_raw(ar.reduce(y)) : ar.canon(y);
+            }
         }
     }
+};
+
+// One launch runs one pass over the whole batch.  Workgroups are persistent: each walks tiles
+// blockIdx.x, blockIdx.x + gridDim.x, ... (gridDim.x a multiple of 8, so a workgroup's tiles all fall
+// in its XCD group's contiguous range of xcd_remap).  PF: the raw loads of the next tile are issued
+// before the butterflies of the current one.
+template <class P, bool PF, class TS>
+__device__ __forceinline__ void pass_loop(const PassArgs<TS>& a, uint64_t* lds) {
+    const P p(a);
+    const uint32_t nb = a.nblocks;
+    uint32_t lt = blockIdx.x;
+    if (lt >= nb) return;
+    TileLoc L = p.locate(xcd_remap(lt, nb));
+    uint64_t raw[P::R];
+    p.load(L, raw);
+    while (true) {
+        const uint32_t nlt = lt + gridDim.x;
+        const bool more = nlt < nb;   // workgroup-uniform
+        TileLoc Ln;
+        uint64_t nraw[PF ? P::R : 1];
+        if constexpr (PF) {
+            if (more) {
+                Ln = p.locate(xcd_remap(nlt, nb));
+                p.load(Ln, nraw);
+            }
+        }
+        p.compute_store(L, raw, lds);
+        if (!more) break;
+        lt = nlt;
+        if constexpr (PF) {
+            L = Ln;
+            for (int k = 0; k < P::R; ++k) raw[k] = nraw[k];   // register renaming, no code
+        } else {
+            L = p.locate(xcd_remap(lt, nb));
+            p.load(L, raw);
+        }
+        // the next tile's first LDS exchange starts with a barrier, so LDS rows are not overwritten early
+    }
+}
+
+template <class A, class TS, int LOG_G, int LOG_R, int NG, bool COLS, bool INV, bool IN_RAW, bool OUT_RAW,
+          bool TWIST, bool BREV, bool UNI, bool PF>
+__global__ __launch_bounds__(NG * (1 << (LOG_G - LOG_R))) void ntt_pass_kernel(PassArgs<TS> a) {
+    extern __shared__ __attribute__((aligned(16))) uint64_t lds[];
+    pass_loop<NttPass<A, TS, LOG_G, LOG_R, NG, COLS, INV, IN_RAW, OUT_RAW, TWIST, BREV, UNI>, PF>(a, lds);
 }
 
 }  // namespace mfhe

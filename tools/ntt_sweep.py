@@ -1,34 +1,66 @@
 #!/usr/bin/env python3
-"""Sweep NTT plan / chunk options on the device (dev tool)."""
-import sys, json
-from pathlib import Path
-ROOT = Path(__file__).resolve().parent.parent
-sys.path.insert(0, str(ROOT / "matrix-fhe-gpu_amd")); sys.path.insert(0, str(ROOT)); sys.path.insert(0, str(ROOT / "tools"))
-import torch
-import mfhe
-from bench import gen_moduli
-from ntt_perf import t_call
+"""Sweep NTT launch options (prefetch, workgroups/CU, chunk bytes) across shapes; HIP-event timing. Dev tool.
 
-MiB = 1 << 20
-cases = [((16, 8, 1024), [(0, c) for c in (0, 16 * MiB, 32 * MiB, 64 * MiB, 96 * MiB, 128 * MiB, 192 * MiB)]),
-         ((15, 8, 1024), [(0, c) for c in (0, 32 * MiB, 64 * MiB, 128 * MiB)]),
-         ((17, 32, 128), [(0, c) for c in (0, 32 * MiB, 64 * MiB, 128 * MiB)]),
-         ((14, 4, 256), [(1, 0), (2, 0), (2, 32 * MiB), (2, 64 * MiB)]),
-         ((14, 4, 2048), [(1, 0), (2, 0), (2, 32 * MiB), (2, 64 * MiB), (2, 128 * MiB)]),
-         ((13, 4, 2048), [(1, 0), (2, 32 * MiB), (2, 64 * MiB)]),
-         ((12, 1, 4096), [(1, 0), (2, 0), (2, 32 * MiB)])]
-for (log_n, L, batch), opts in cases:
-    N = 1 << log_n
-    ctx = mfhe.Context(gen_moduli(50, 1 << (log_n + 2), L), log_n)
-    d = torch.randint(0, 2 ** 40, (batch * L * N,), dtype=torch.int64, device="cuda")
-    for plan, chunk in opts:
-        ctx.set_option(mfhe.OPT_NTT_PLAN, plan)
-        ctx.set_option(mfhe.OPT_NTT_CHUNK_BYTES, chunk)
-        f = t_call(lambda: ctx.ntt_fwd(d, batch=batch))
-        i = t_call(lambda: ctx.ntt_inv(d, batch=batch))
-        nt = batch * L
-        print(json.dumps({"logN": log_n, "L": L, "batch": batch, "plan": plan, "chunk_MiB": chunk // MiB,
-                          "fwd_ms": round(f, 4), "fwd_NTT_s": round(nt / f * 1e3),
-                          "fwd_alg_GBps": round(16.0 * N * nt / f / 1e6, 1), "inv_ms": round(i, 4)}), flush=True)
-    del d
-    torch.cuda.empty_cache()
+usage: tools/ntt_sweep.py [logN,L,batch ...]   (one JSON line per configuration)
+"""
+import json
+import sys
+from pathlib import Path
+
+ROOT = Path(__file__).resolve().parent.parent
+sys.path.insert(0, str(ROOT / "matrix-fhe-gpu_amd"))
+sys.path.insert(0, str(ROOT))
+import torch  # noqa: E402
+
+import mfhe  # noqa: E402
+from bench import gen_moduli  # noqa: E402
+
+OPT_WG, OPT_PF = 4, 5
+
+
+def t_call(fn, reps=8):
+    fn()
+    torch.cuda.synchronize()
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    e0.record()
+    for _ in range(reps):
+        fn()
+    e1.record()
+    torch.cuda.synchronize()
+    return e0.elapsed_time(e1) / reps
+
+
+def main():
+    shapes = [(16, 8, 1024), (14, 4, 256), (17, 32, 128), (12, 1, 4096), (6, 11, 32768)]
+    if len(sys.argv) > 1:
+        shapes = [tuple(int(x) for x in a.split(",")) for a in sys.argv[1:]]
+    for log_n, L, batch in shapes:
+        N = 1 << log_n
+        mods = mfhe.RNS_MODULI if (log_n == 6 and L == 11) else gen_moduli(50, 1 << (log_n + 2), L)
+        ctx = mfhe.Context(mods, log_n)
+        q = torch.tensor(mods, dtype=torch.int64, device="cuda").repeat_interleave(N).repeat(batch)
+        d = torch.randint(0, 2 ** 62, (batch * L * N,), dtype=torch.int64, device="cuda") % q
+        ref = d.clone()
+        chunks = [192 << 20, 0] if log_n > 14 else [192 << 20]
+        for pf in (0, 1):
+            for wg in (0, 1, 2, 3, 4):
+                for cb in chunks:
+                    ctx.set_option(OPT_PF, pf)
+                    ctx.set_option(OPT_WG, wg)
+                    ctx.set_option(mfhe.OPT_NTT_CHUNK_BYTES, cb)
+                    ctx.ntt_fwd(d, batch=batch)
+                    ctx.ntt_inv(d, batch=batch)
+                    torch.cuda.synchronize()
+                    ok = bool(torch.equal(d, ref))
+                    f = t_call(lambda: ctx.ntt_fwd(d, batch=batch))
+                    i = t_call(lambda: ctx.ntt_inv(d, batch=batch))
+                    ntts = batch * L
+                    print(json.dumps({"logN": log_n, "L": L, "batch": batch, "prefetch": pf, "wg_per_cu": wg,
+                                      "chunk_MiB": cb >> 20, "fwd_ms": round(f, 4), "fwd_NTT_s": round(ntts / f * 1e3),
+                                      "fwd_alg_GBps": round(16 * N * ntts / f / 1e6, 1), "inv_ms": round(i, 4),
+                                      "inv_NTT_s": round(ntts / i * 1e3), "roundtrip_ok": ok}), flush=True)
+        del d, ref, q
+
+
+if __name__ == "__main__":
+    main()
