@@ -47,16 +47,22 @@ struct ArithF64 {
     __device__ __forceinline__ static double from_raw(uint64_t x) { return __longlong_as_double((long long)x); }
     __device__ __forceinline__ static uint64_t to_raw(double x) { return (uint64_t)__double_as_longlong(x); }
 
-    // t = v*w mod q, |t| <= q/2 + |v||w| 2^-53 (exact integer in a double)
+    // Round-to-integer by the 1.5*2^52 magic constant: fma(a, b, C) - C = nearest integer to a*b for
+    // |a*b| < 2^51, two full-rate FP64 ops (v_rndne_f64 is not full rate on gfx950).  The quotient
+    // only has to be within +-1 of v*w/q for the bounds below; canonical outputs do not depend on it.
+    static constexpr double kMagic = 6755399441055744.0;   // 1.5 * 2^52
+    __device__ __forceinline__ static double round_int(double a, double b) { return __fma_rn(a, b, kMagic) - kMagic; }
+
+    // t = v*w mod q, |t| <= q/2 + |v||w| 2^-53 (exact integer in a double); needs |v w / q| < 2^51
     __device__ __forceinline__ double mulmod(double v, Tw w) const {
         double hi = v * w.x;
         double lo = __fma_rn(v, w.x, -hi);
-        double k = __builtin_rint(v * w.y);
+        double k = round_int(v, w.y);
         return __fma_rn(-k, q, hi) + lo;
     }
-    // centred reduction: |result| <= q/2 (+ negligible) for |x| < 2^53
+    // centred reduction: |result| <= q/2 (+ negligible) for |x| < 2^51 q
     __device__ __forceinline__ double reduce(double x) const {
-        return __fma_rn(-__builtin_rint(x * qinv), q, x);
+        return __fma_rn(-round_int(x, qinv), q, x);
     }
     // Cooley-Tukey: (u, v) <- (u + wv, u - wv)
     __device__ __forceinline__ void ct(double& u, double& v, Tw w) const {
@@ -75,10 +81,8 @@ struct ArithF64 {
     __device__ __forceinline__ double round_reduce(double x) const { return reduce(x); }
     // exact canonical u64 in [0, q)
     __device__ __forceinline__ uint64_t canon(double x) const {
-        double k = __builtin_floor(x * qinv);
-        double r = __fma_rn(-k, q, x);
-        r = (r < 0.0) ? r + q : r;
-        r = (r >= q) ? r - q : r;
+        double r = reduce(x);          // |r| <= q/2 + eps
+        r = (r < 0.0) ? r + q : r;     // [0, q)
         return (uint64_t)__double_as_longlong(r + kTwo52) & 0x000FFFFFFFFFFFFFULL;
     }
 };
