@@ -61,8 +61,8 @@ struct mfhe_ctx {
     std::vector<uint64_t> moduli;
     int64_t ntt_chunk_bytes = 192ll << 20;  // measured best at N = 2^15..2^17 (profiles/r01_ntt_sweep.txt)
     int ntt_plan = 0;
-    int ntt_wg_per_cu = 0;
-    int ntt_prefetch = 0;    // persistent NTT passes: prefetch the next tile's raw data (MFHE_OPT_NTT_PREFETCH)   // persistent NTT grid: workgroups per CU (0 = occupancy limit)
+    int ntt_wg_per_cu = 16;  // NTT pass grid: workgroups per CU (0 = occupancy, 16 = one tile per WG; measured best)
+    int ntt_prefetch = 0;    // persistent NTT passes: prefetch the next tile's raw data (MFHE_OPT_NTT_PREFETCH)
     int num_cus = 256;
 
     mfhe::LimbConst* d_limbs = nullptr;  // [L]
