@@ -39,6 +39,7 @@ def parse():
     ap.add_argument("--ntt-wg", type=int, default=None, help="MFHE_OPT_NTT_WG_PER_CU override (tuning)")
     ap.add_argument("--ntt-prefetch", type=int, default=None, help="MFHE_OPT_NTT_PREFETCH override (tuning)")
     ap.add_argument("--ntt-chunk", type=int, default=None, help="MFHE_OPT_NTT_CHUNK_BYTES override (tuning)")
+    ap.add_argument("--ntt-fused", type=int, default=None, help="MFHE_OPT_NTT_FUSED override (tuning)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-seconds", type=float, default=10.0)
     ap.add_argument("--only", default="all", help="all | ntt | crt | recombine (profiling)")
@@ -129,7 +130,8 @@ def main():
     ctx = mfhe.Context(moduli, log_n, mfhe.CONV_PHANTOM)
     if args.arith:
         ctx.set_arith(args.arith)
-    for opt, val in ((4, args.ntt_wg), (5, args.ntt_prefetch), (mfhe.OPT_NTT_CHUNK_BYTES, args.ntt_chunk)):
+    for opt, val in ((4, args.ntt_wg), (5, args.ntt_prefetch), (mfhe.OPT_NTT_CHUNK_BYTES, args.ntt_chunk),
+                     (6, args.ntt_fused)):
         if val is not None:
             ctx.set_option(opt, val)
     stream = torch.cuda.current_stream()
@@ -186,28 +188,38 @@ def main():
         res["crt_ev_ms"], res["crt_batch"] = ev_c, cb
 
     if args.only in ("all", "recombine") and args.recombine_batch and L % world == 0:
-        # residue sharding: rank g owns limbs [g*L/G, (g+1)*L/G) of every poly; one step =
-        # INTT of the shard + RCCL exchange + sharded CRT compose of this rank's batch slice -> f64.
+        # residue sharding: rank g owns limbs [g*L/G, (g+1)*L/G) of every poly.  One step =
+        # forward + inverse NTT of the shard (a computation round trip) + RCCL exchange + sharded CRT
+        # compose of this rank's batch slice -> f64.  The shard holds RNS residues of real messages
+        # (|z| < 1 scaled by delta), as a decode does.
         from mfhe import dist as mdist
         rb = max(world, args.recombine_batch // world * world)
         s0, lg = mdist.limb_range(L, world, rank)
-        shard = torch.empty(rb * lg * N, dtype=torch.int64, device=dev).random_(0, 2 ** 62, generator=g)
-        shard.remainder_(torch.tensor(moduli[s0:s0 + lg], dtype=torch.int64, device=dev).repeat_interleave(N).repeat(rb))
+        full = torch.empty(rb * L * N, dtype=torch.int64, device=dev)
+        zr = torch.rand(rb * N, dtype=torch.float64, device=dev, generator=g) * 2 - 1
+        ctx.rns_decompose(zr, full, rb, N, stream=stream)
+        shard = full.view(rb, L, N)[:, s0:s0 + lg, :].contiguous().view(-1)
+        del full, zr
         rout = torch.empty(rb // world * N, dtype=torch.float64, device=dev)
         rc = {}
+        nrep = max(1, args.steps // 4)
         modes = ("allgather", "alltoall") if world > 1 else ("local",)
         for mode in modes:
             def step(mode=mode):
+                ctx.ntt_fwd(shard, batch=rb, start_limb=s0, nlimbs=lg, stream=stream)
                 ctx.ntt_inv(shard, batch=rb, start_limb=s0, nlimbs=lg, stream=stream)
                 if mode == "local":
                     ctx.crt_compose_f64(shard, rout, rb, N, stream=stream)
                 else:
                     mdist.crt_recombine(ctx, shard, rb, N, mode, out=rout, stream=stream)
-            w_r, ev_r = timed(step, max(1, args.steps // 4), 1)
-            rc[mode] = w_r / max(1, args.steps // 4)
-        w_n, _ = timed(lambda: ctx.ntt_inv(shard, batch=rb, start_limb=s0, nlimbs=lg, stream=stream),
-                       max(1, args.steps // 4), 1)
-        res["recombine"] = {"batch": rb, "limbs_per_gpu": lg, "intt_only_ms": w_n / max(1, args.steps // 4) * 1e3,
+            w_r, _ = timed(step, nrep, 1)
+            rc[mode] = w_r / nrep
+
+        def ntt_rt():
+            ctx.ntt_fwd(shard, batch=rb, start_limb=s0, nlimbs=lg, stream=stream)
+            ctx.ntt_inv(shard, batch=rb, start_limb=s0, nlimbs=lg, stream=stream)
+        w_n, _ = timed(ntt_rt, nrep, 1)
+        res["recombine"] = {"batch": rb, "limbs_per_gpu": lg, "ntt_roundtrip_only_ms": w_n / nrep * 1e3,
                             **{f"{m}_ms": t * 1e3 for m, t in rc.items()},
                             **{f"{m}_polys_per_s": rb / t for m, t in rc.items()}}
 
@@ -248,7 +260,7 @@ def main():
             out["encode_crt_ops_per_s"] = cb / (res["crt_ev_ms"] * 1e-3) * world
             out["encode_crt_GBps"] = 16.0 * (L + 1) * N * cb / (res["crt_ev_ms"] * 1e-3) / 1e9
         if "recombine" in res:
-            out["residue_shard_intt_crt_recombine"] = res["recombine"]
+            out["residue_shard_ntt_roundtrip_crt_recombine"] = res["recombine"]
         if world == 1 and not args.no_cpu_baseline and args.only == "all":
             try:
                 out["cpu_baseline"] = cpu_baseline(log_n, moduli, args.cpu_seconds)

@@ -48,11 +48,11 @@ __global__ __launch_bounds__(256) void rns_decompose_kernel(const double* __rest
 // shard_stride = 0 is the plain [npoly][L][ncoeff] layout; Lg < L reads residue shards gathered from
 // several GPUs ([shard][npoly][Lg][ncoeff]) in place, without a transpose.
 template <int W>
-__device__ __forceinline__ void compose_one(const uint64_t* __restrict__ in, uint64_t ncoeff, int L, int Lg,
-                                            uint64_t shard_stride, const uint64_t* __restrict__ qmu,
-                                            const uint64_t* __restrict__ inv, const double* __restrict__ qinv,
-                                            const uint64_t* __restrict__ M, const uint64_t* __restrict__ Q,
-                                            const uint64_t* __restrict__ Qh, uint64_t (&mag)[W], bool& neg) {
+__device__ __forceinline__ void compose_slow(const uint64_t* __restrict__ in, uint64_t ncoeff, int L, int Lg,
+                                          uint64_t shard_stride, const uint64_t* __restrict__ qmu,
+                                          const uint64_t* __restrict__ inv, const double* __restrict__ qinv,
+                                          const uint64_t* __restrict__ M, const uint64_t* __restrict__ Q,
+                                          const uint64_t* __restrict__ Qh, uint64_t (&mag)[W], bool& neg) {
     uint64_t acc[W + 1];
 #pragma unroll
     for (int i = 0; i <= W; ++i) acc[i] = 0;
@@ -139,6 +139,67 @@ __device__ __forceinline__ void compose_one(const uint64_t* __restrict__ in, uin
 #pragma unroll
         for (int i = 0; i < W; ++i) mag[i] = acc[i];
     }
+}
+
+// Small-value fast path.  With u = nearest integer to sum_k t_k/q_k, the centred CRT value is
+// X = sum_k t_k M_k - u Q; its low 64 bits cost one wrapping multiply-add per limb.  The candidate
+// c = (int64) low64(X) is accepted only if |c| <= Q_half and c = x_k (mod q_k) for every k: by CRT
+// uniqueness it then IS the centred value, bit-identical to compose_slow.  Decoded messages (|X| ~
+// delta * |m| + noise) always take it; inputs that fail the check (random residues) take the full
+// W-word path.
+template <int W>
+__device__ __forceinline__ void compose_one(const uint64_t* __restrict__ in, uint64_t ncoeff, int L, int Lg,
+                                            uint64_t shard_stride, const uint64_t* __restrict__ qmu,
+                                            const uint64_t* __restrict__ inv, const double* __restrict__ qinv,
+                                            const uint64_t* __restrict__ M, const uint64_t* __restrict__ Q,
+                                            const uint64_t* __restrict__ Qh, uint64_t (&mag)[W], bool& neg) {
+    uint64_t lo = 0;
+    double est = 0.0;
+    {
+        const uint64_t* p = in;
+        for (int k = 0, j = 0; k < L; ++k) {
+            const uint64_t q = qmu[2 * k];
+            const uint64_t x = p[(uint64_t)j * ncoeff];
+            if (++j == Lg) {
+                j = 0;
+                p += shard_stride;
+            }
+            uint64_t t = x * inv[2 * k] - __umul64hi(x, inv[2 * k + 1]) * q;   // Shoup: [0, 2q)
+            t = t >= q ? t - q : t;
+            est += (double)t * qinv[k];
+            lo += t * M[(size_t)k * W];                                       // wrapping
+        }
+    }
+    const uint64_t u = (uint64_t)__builtin_rint(est);
+    const int64_t c = (int64_t)(lo - u * Q[0]);
+    const uint64_t a = c < 0 ? (uint64_t)0 - (uint64_t)c : (uint64_t)c;
+    bool qbig = false;   // Q_half >= 2^64: every |c| < 2^62 is inside (-Q/2, Q/2)
+#pragma unroll
+    for (int i = 1; i < W; ++i) qbig |= Qh[i] != 0;
+    bool ok = a < (1ull << 62) && (qbig || a <= Qh[0]);
+    {
+        const uint64_t* p = in;
+        for (int k = 0, j = 0; k < L && ok; ++k) {
+            const uint64_t q = qmu[2 * k], mu = qmu[2 * k + 1];
+            const uint64_t x = p[(uint64_t)j * ncoeff];
+            if (++j == Lg) {
+                j = 0;
+                p += shard_stride;
+            }
+            uint64_t r = a - __umul64hi(a, mu) * q;   // Barrett: [0, 2q)
+            r = r >= q ? r - q : r;
+            r = (c < 0 && r) ? q - r : r;
+            ok = r == x;
+        }
+    }
+    if (ok) {
+        mag[0] = a;
+#pragma unroll
+        for (int i = 1; i < W; ++i) mag[i] = 0;
+        neg = c < 0;
+        return;
+    }
+    compose_slow<W>(in, ncoeff, L, Lg, shard_stride, qmu, inv, qinv, M, Q, Qh, mag, neg);
 }
 
 template <int W>

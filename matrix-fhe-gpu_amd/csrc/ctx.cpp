@@ -402,6 +402,7 @@ extern "C" int mfhe_ctx_create(const uint64_t* moduli, int L, int log_n, int con
 extern "C" int mfhe_ctx_destroy(mfhe_ctx* c) {
     if (!c) return MFHE_OK;
     if (c->ws) (void)hipFree(c->ws);
+    if (c->fused_buf) (void)hipFree(c->fused_buf);
     for (void* p : c->allocs) (void)hipFree(p);
     delete c;
     return MFHE_OK;
@@ -448,6 +449,14 @@ extern "C" int mfhe_ctx_set_option(mfhe_ctx* c, int opt, int64_t v) {
             if (v < 0 || v > 1) return set_error(MFHE_EINVAL, "prefetch must be 0 or 1");
             c->ntt_prefetch = (int)v;
             return MFHE_OK;
+        case MFHE_OPT_NTT_FUSED:
+            if (v < 0 || v > 1) return set_error(MFHE_EINVAL, "fused must be 0 or 1");
+            c->ntt_fused = (int)v;
+            return MFHE_OK;
+        case MFHE_OPT_NTT_FUSED_LAG:
+            if (v < 1 || v > 64) return set_error(MFHE_EINVAL, "fused lag must be in [1, 64]");
+            c->ntt_fused_lag = (int)v;
+            return MFHE_OK;
         case MFHE_OPT_CRT_WORDS:
             if (v < 1 || v > 32) return set_error(MFHE_EINVAL, "crt words must be in [1, 32]");
             if (v <= c->W) return MFHE_OK;
@@ -482,6 +491,19 @@ extern "C" int mfhe_ctx_get_option(const mfhe_ctx* c, int opt, int64_t* v) {
         case MFHE_OPT_NTT_PLAN: *v = c->ntt_plan; return MFHE_OK;
         case MFHE_OPT_NTT_WG_PER_CU: *v = c->ntt_wg_per_cu; return MFHE_OK;
         case MFHE_OPT_NTT_PREFETCH: *v = c->ntt_prefetch; return MFHE_OK;
+        case MFHE_OPT_NTT_FUSED: *v = c->ntt_fused; return MFHE_OK;
+        case MFHE_OPT_NTT_FUSED_LAG: *v = c->ntt_fused_lag; return MFHE_OK;
+        case MFHE_OPT_NTT_FUSED_ERRORS: {
+            // synchronous: the error word of the last fused launch (0 = no spin timed out)
+            uint32_t e = 0;
+            if (c->fused_buf) {
+                hipError_t he = hipDeviceSynchronize();
+                if (he == hipSuccess) he = hipMemcpy(&e, (const char*)c->fused_buf + 16 * 128 + 4, 4, hipMemcpyDeviceToHost);
+                if (he != hipSuccess) return hip_error(he, "fused error word");
+            }
+            *v = e;
+            return MFHE_OK;
+        }
         case MFHE_OPT_CRT_WORDS: *v = c->W; return MFHE_OK;
         default: return set_error(MFHE_EINVAL, "unknown option");
     }

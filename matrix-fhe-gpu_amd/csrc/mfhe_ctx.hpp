@@ -64,6 +64,10 @@ struct mfhe_ctx {
     int ntt_wg_per_cu = 16;  // NTT pass grid: workgroups per CU (0 = occupancy, 16 = one tile per WG; measured best)
     int ntt_prefetch = 0;    // persistent NTT passes: prefetch the next tile's raw data (MFHE_OPT_NTT_PREFETCH)
     int num_cus = 256;
+    int ntt_fused = 0;       // N = 2^15..2^17: both passes in one launch (MFHE_OPT_NTT_FUSED)
+    int ntt_fused_lag = 2;   // pass-2 lag in polynomials per XCD queue
+    void* fused_buf = nullptr;   // FusedSync + map/arr arrays, grown on demand
+    size_t fused_bytes = 0;
 
     mfhe::LimbConst* d_limbs = nullptr;  // [L]
     uint64_t* d_dmod = nullptr;          // [L][3] phantom DModulus {value, const_ratio[2]}

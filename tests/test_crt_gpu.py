@@ -131,3 +131,39 @@ def test_crt_compose_f64_sharded_matches_unsharded(mfhe, orc, world):
         ctx.crt_compose_f64_sharded(mfhe.to_device_u64(a2a), got, world, bs * lg * N, bs, N)
         torch.cuda.synchronize()
         assert torch.equal(got, ref)
+
+
+@pytest.mark.parametrize("L,W", [(1, None), (1, 7), (2, None), (8, None), (11, 7)])
+def test_crt_compose_small_value_fast_path_boundaries(mfhe, orc, L, W):
+    """Centred values around the fast path's limits (|X| near 2^62, near Q/2 for small Q) must match the
+    full multi-word compose bit-exactly (oracle), whichever path the kernel takes."""
+    import torch
+    moduli = RNS[:L] if L == 11 else orc.gen_primes(50, 1 << 18, L)
+    Q = 1
+    for q in moduli:
+        Q *= q
+    vals = [0, 1, -1, 2 ** 35, -(2 ** 35) - 7, 2 ** 52 + 1, -(2 ** 53), 2 ** 62 - 1, -(2 ** 62 - 1), 2 ** 62, -(2 ** 62),
+            2 ** 63 - 1, -(2 ** 63 - 1), 2 ** 64 + 3, -(2 ** 70)]
+    half = (Q - 1) // 2
+    vals += [half, -half, half - 1, -(half - 1)]
+    vals = [v for v in vals if abs(v) <= half]
+    nc = len(vals)
+    res = np.array([[v % q for v in vals] for q in moduli], dtype=np.uint64).ravel()
+    ctx = mfhe.Context(moduli, 6, mfhe.CONV_PHANTOM)
+    if W:
+        ctx.set_option(mfhe.OPT_CRT_WORDS, W)
+    Wc = ctx.info().crt_words
+    d = mfhe.to_device_u64(res)
+    mag = torch.empty(nc * Wc, dtype=torch.int64, device="cuda")
+    neg = torch.empty(nc, dtype=torch.uint8, device="cuda")
+    ctx.crt_compose(d, mag, neg, 1, nc)
+    f = torch.empty(nc, dtype=torch.float64, device="cuda")
+    ctx.crt_compose_f64(d, f, 1, nc)
+    torch.cuda.synchronize()
+    m_ref, n_ref = orc.crt_compose(res, 1, L, nc, moduli, W=Wc)
+    np.testing.assert_array_equal(mfhe.to_host_u64(mag).reshape(nc, Wc), m_ref)
+    np.testing.assert_array_equal(neg.cpu().numpy(), n_ref)
+    np.testing.assert_array_equal(f.cpu().numpy(), orc.big_to_f64(m_ref, n_ref, Wc, 2.0 ** 35))
+    for i, v in enumerate(vals):   # and the value itself
+        got = sum(int(w) << (64 * j) for j, w in enumerate(m_ref[i]))
+        assert (-got if n_ref[i] else got) == v

@@ -15,7 +15,7 @@ import torch  # noqa: E402
 import mfhe  # noqa: E402
 from bench import gen_moduli  # noqa: E402
 
-OPT_WG, OPT_PF = 4, 5
+OPT_WG, OPT_PF, OPT_FUSED, OPT_LAG = 4, 5, 6, 7
 
 
 def t_call(fn, reps=8):
@@ -42,6 +42,22 @@ def main():
         d = torch.randint(0, 2 ** 62, (batch * L * N,), dtype=torch.int64, device="cuda") % q
         ref = d.clone()
         chunks = [192 << 20, 0] if log_n > 14 else [192 << 20]
+        if log_n >= 15:
+            for lag in (1, 2, 3, 4, 6):
+                ctx.set_option(OPT_FUSED, 1)
+                ctx.set_option(OPT_LAG, lag)
+                ctx.ntt_fwd(d, batch=batch)
+                ctx.ntt_inv(d, batch=batch)
+                torch.cuda.synchronize()
+                ok = bool(torch.equal(d, ref)) and ctx.get_option(8) == 0
+                f = t_call(lambda: ctx.ntt_fwd(d, batch=batch))
+                i = t_call(lambda: ctx.ntt_inv(d, batch=batch))
+                ntts = batch * L
+                print(json.dumps({"logN": log_n, "L": L, "batch": batch, "fused": 1, "lag": lag, "fwd_ms": round(f, 4),
+                                  "fwd_NTT_s": round(ntts / f * 1e3), "fwd_alg_GBps": round(16 * N * ntts / f / 1e6, 1),
+                                  "inv_ms": round(i, 4), "inv_NTT_s": round(ntts / i * 1e3), "roundtrip_ok": ok}),
+                      flush=True)
+            ctx.set_option(OPT_FUSED, 0)
         import os
         quick = os.environ.get("QUICK") == "1"
         for pf in ((0,) if quick else (0, 1)):
