@@ -71,7 +71,7 @@ static void build_ct_tables(uint64_t q, uint64_t psi, int logN, uint64_t* tw, ui
 
 struct HostTabs {
     std::vector<uint64_t> tw, tws, itw, itws, ninv, ninvs;
-    std::vector<double2> twf, itwf, ninvf;
+    std::vector<double> twf, itwf, ninvf;   // centred w (the FP64 quotient uses (v*w)/q)
 };
 
 static void add_limb_tables(HostTabs& h, uint64_t q, uint64_t psi, int logN, bool f64) {
@@ -86,15 +86,15 @@ static void add_limb_tables(HostTabs& h, uint64_t q, uint64_t psi, int logN, boo
         h.itws.push_back(hm::shoup(itw[i], q));
         if (f64) {
             double a = centred(tw[i], q), b = centred(itw[i], q);
-            h.twf.push_back(make_double2(a, a / (double)q));
-            h.itwf.push_back(make_double2(b, b / (double)q));
+            h.twf.push_back(a);
+            h.itwf.push_back(b);
         }
     }
     h.ninv.push_back(ninv);
     h.ninvs.push_back(hm::shoup(ninv, q));
     if (f64) {
         double a = centred(ninv, q);
-        h.ninvf.push_back(make_double2(a, a / (double)q));
+        h.ninvf.push_back(a);
     }
 }
 
@@ -110,16 +110,16 @@ static int upload_tabs(mfhe_ctx* c, HostTabs& h, NttTablesU& u, NttTablesF& f) {
     return MFHE_OK;
 }
 
-// powers table: out[j] = r^j, both u64 (+shoup) and F64 pairs
+// powers table: out[j] = r^j, u64 (+shoup) and centred F64
 static void powers(uint64_t q, uint64_t r, size_t n, bool f64, std::vector<uint64_t>& w, std::vector<uint64_t>& ws,
-                   std::vector<double2>& wf) {
+                   std::vector<double>& wf) {
     uint64_t c = 1;
     for (size_t j = 0; j < n; ++j) {
         w.push_back(c);
         ws.push_back(hm::shoup(c, q));
         if (f64) {
             double a = centred(c, q);
-            wf.push_back(make_double2(a, a / (double)q));
+            wf.push_back(a);
         }
         c = hm::mulmod(c, r, q);
     }
@@ -344,7 +344,7 @@ static int ctx_create_impl(const uint64_t* moduli, int L, int logN, int conv, do
     if (conv & MFHE_CONV_GL) {
         HostTabs h;
         std::vector<uint64_t> gpre, gpres, gpost, gposts, cpre, cpres, cpost, cposts;
-        std::vector<double2> gpref, gpostf, cpref, cpostf;
+        std::vector<double> gpref, gpostf, cpref, cpostf;
         for (int i = 0; i < L; ++i) {
             const uint64_t q = moduli[i];
             const uint64_t beta = hm::first_psi4n(q, N);

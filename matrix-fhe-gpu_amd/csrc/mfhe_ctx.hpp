@@ -33,10 +33,10 @@ int ensure_xy(mfhe_ctx* c);   // XY encoder matrices, built on first use (ctx.cp
         if (_e != hipSuccess) return ::mfhe::hip_error(_e, what); \
     } while (0)
 
-struct NttTablesF {   // FP64 path: (w centred, w/q) pairs
-    double2* tw = nullptr;    // [L][N]
-    double2* itw = nullptr;   // [L][N], itw[1] *= n^-1
-    double2* ninv = nullptr;  // [L]
+struct NttTablesF {   // FP64 path: centred w
+    double* tw = nullptr;    // [L][N]
+    double* itw = nullptr;   // [L][N], itw[1] *= n^-1
+    double* ninv = nullptr;  // [L]
 };
 struct NttTablesU {   // U64 path / phantom format
     uint64_t* tw = nullptr;     // [L][N]
@@ -78,7 +78,7 @@ struct mfhe_ctx {
     // GL / cyclic tables (network root psi' = beta^2, beta = first-found psi4n)
     mfhe::NttTablesF gl_f;
     mfhe::NttTablesU gl_u;
-    double2 *gl_pre_f = nullptr, *gl_post_f = nullptr, *cyc_pre_f = nullptr, *cyc_post_f = nullptr;  // [L][N]
+    double *gl_pre_f = nullptr, *gl_post_f = nullptr, *cyc_pre_f = nullptr, *cyc_post_f = nullptr;  // [L][N]
     uint64_t *gl_pre_u = nullptr, *gl_pre_us = nullptr, *gl_post_u = nullptr, *gl_post_us = nullptr;
     uint64_t *cyc_pre_u = nullptr, *cyc_pre_us = nullptr, *cyc_post_u = nullptr, *cyc_post_us = nullptr;
     uint32_t *gl_perm = nullptr, *gl_inv_perm = nullptr;  // [N]

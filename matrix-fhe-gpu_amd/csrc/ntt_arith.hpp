@@ -34,7 +34,7 @@ struct LimbConst {
 
 struct ArithF64 {
     using T = double;
-    using Tw = double2;      // (w, w/q), w centred in (-q/2, q/2]
+    using Tw = double;       // w centred in (-q/2, q/2]
     double q, qinv;
 
     __device__ __forceinline__ explicit ArithF64(const LimbConst& c) : q(c.qf), qinv(c.qinv) {}
@@ -53,11 +53,13 @@ struct ArithF64 {
     static constexpr double kMagic = 6755399441055744.0;   // 1.5 * 2^52
     __device__ __forceinline__ static double round_int(double a, double b) { return __fma_rn(a, b, kMagic) - kMagic; }
 
-    // t = v*w mod q, |t| <= q/2 + |v||w| 2^-53 (exact integer in a double); needs |v w / q| < 2^51
+    // t = v*w mod q (exact integer in a double): hi + lo = v*w exactly, k = round(hi / q) (within 1 of
+    // v*w/q), t = (hi - k q) + lo; needs |v w / q| < 2^51.  The quotient comes from hi, so the twiddle
+    // table holds w alone (8 B per entry instead of a (w, w/q) pair).
     __device__ __forceinline__ double mulmod(double v, Tw w) const {
-        double hi = v * w.x;
-        double lo = __fma_rn(v, w.x, -hi);
-        double k = round_int(v, w.y);
+        double hi = v * w;
+        double lo = __fma_rn(v, w, -hi);
+        double k = round_int(hi, qinv);
         return __fma_rn(-k, q, hi) + lo;
     }
     // centred reduction: |result| <= q/2 (+ negligible) for |x| < 2^51 q

@@ -31,8 +31,8 @@
 namespace mfhe {
 
 struct TwSrcF {
-    const double2* p;
-    __device__ __forceinline__ double2 get(size_t i) const { return p[i]; }
+    const double* p;
+    __device__ __forceinline__ double get(size_t i) const { return p[i]; }
 };
 struct TwSrcU {
     const uint64_t* w;
