@@ -18,6 +18,7 @@
 #include <vector>
 
 #include "host_math.hpp"
+#include "gemm.hpp"
 #include "mfhe_ctx.hpp"
 
 namespace mfhe {
@@ -231,6 +232,39 @@ static int build_wcrt(mfhe_ctx* c) {
     if ((rc = upload(c, &c->d_wV, V)) || (rc = upload(c, &c->d_wVinv, Vi)) || (rc = upload(c, &c->d_wdV, wdv)) ||
         (rc = upload(c, &c->d_wdVinv, wdvi)))
         return rc;
+    // i8 MFMA operand planes (gemm.hip): D balanced base-256 digits of every V / V^-1 entry, and
+    // 256^s mod q for the epilogue.  Needs 2^27 < q (|acc_s| < q) and q < 2^59 (D <= 8).
+    int bits = 0;
+    bool big = true;
+    for (uint64_t q : c->moduli) {
+        bits = std::max(bits, 64 - __builtin_clzll(q));
+        big = big && q > (1ull << 27);
+    }
+    const int D = std::max(5, (bits + 1 + 7) / 8);
+    if (big && D <= 8) {
+        const size_t plane = (size_t)PHI * PHI;
+        std::vector<int8_t> vd((size_t)L * D * plane), vid((size_t)L * D * plane);
+        std::vector<uint64_t> rt((size_t)L * (2 * D - 1) * 2);
+        for (int l = 0; l < L; ++l) {
+            int8_t d[8];
+            for (size_t e = 0; e < plane; ++e) {
+                balanced_digits(V[(size_t)l * plane + e], D, d);
+                for (int i = 0; i < D; ++i) vd[((size_t)l * D + i) * plane + e] = d[i];
+                balanced_digits(Vi[(size_t)l * plane + e], D, d);
+                for (int i = 0; i < D; ++i) vid[((size_t)l * D + i) * plane + e] = d[i];
+            }
+            const uint64_t q = c->moduli[l];
+            uint64_t p256 = 1;
+            for (int s = 0; s < 2 * D - 1; ++s) {
+                rt[((size_t)l * (2 * D - 1) + s) * 2] = p256;
+                rt[((size_t)l * (2 * D - 1) + s) * 2 + 1] = hm::shoup(p256, q);
+                p256 = hm::mulmod(p256, 256 % q, q);
+            }
+        }
+        if ((rc = upload(c, &c->d_wVdig, vd)) || (rc = upload(c, &c->d_wVidig, vid)) || (rc = upload(c, &c->d_wrtab, rt)))
+            return rc;
+        c->wD = D;
+    }
     return MFHE_OK;
 }
 
@@ -403,6 +437,7 @@ extern "C" int mfhe_ctx_destroy(mfhe_ctx* c) {
     if (!c) return MFHE_OK;
     if (c->ws) (void)hipFree(c->ws);
     if (c->fused_buf) (void)hipFree(c->fused_buf);
+    if (c->gemm_ws) (void)hipFree(c->gemm_ws);
     for (void* p : c->allocs) (void)hipFree(p);
     delete c;
     return MFHE_OK;
@@ -457,6 +492,10 @@ extern "C" int mfhe_ctx_set_option(mfhe_ctx* c, int opt, int64_t v) {
             if (v < 1 || v > 64) return set_error(MFHE_EINVAL, "fused lag must be in [1, 64]");
             c->ntt_fused_lag = (int)v;
             return MFHE_OK;
+        case MFHE_OPT_WCRT_MFMA:
+            if (v < 0 || v > 1) return set_error(MFHE_EINVAL, "wcrt mfma must be 0 or 1");
+            c->wcrt_mfma = (int)v;
+            return MFHE_OK;
         case MFHE_OPT_CRT_WORDS:
             if (v < 1 || v > 32) return set_error(MFHE_EINVAL, "crt words must be in [1, 32]");
             if (v <= c->W) return MFHE_OK;
@@ -492,6 +531,7 @@ extern "C" int mfhe_ctx_get_option(const mfhe_ctx* c, int opt, int64_t* v) {
         case MFHE_OPT_NTT_WG_PER_CU: *v = c->ntt_wg_per_cu; return MFHE_OK;
         case MFHE_OPT_NTT_PREFETCH: *v = c->ntt_prefetch; return MFHE_OK;
         case MFHE_OPT_NTT_FUSED: *v = c->ntt_fused; return MFHE_OK;
+        case MFHE_OPT_WCRT_MFMA: *v = c->wcrt_mfma && c->d_wVdig; return MFHE_OK;
         case MFHE_OPT_NTT_FUSED_LAG: *v = c->ntt_fused_lag; return MFHE_OK;
         case MFHE_OPT_NTT_FUSED_ERRORS: {
             // synchronous: the error word of the last fused launch (0 = no spin timed out)

@@ -148,7 +148,140 @@ __global__ __launch_bounds__(NTH) void cgemm_kernel(CGemmArgs a) {
     }
 }
 
+// ---------------- i8 MFMA modular GEMM (W-CRT, M = K = 512) ----------------
+//
+// Exact integer product through v_mfma_i32_32x32x32_i8: every operand x < q < 2^(8D-1) is written in
+// D balanced base-256 digits x = sum_i d_i 256^i, d_i in [-128, 127].  For each s = i + j the
+// digit-pair products accumulate in one i32 tile acc_s = sum_{i+j=s} A_i B_j (|acc_s| <= D * 2^14 * 512
+// < 2^26 for D <= 8, exact), and the epilogue folds C = sum_s acc_s * (256^s mod q) mod q.
+// A's digit planes are built once per context; B is split by mfma_digitize_kernel into a
+// [L][D][Ppad][K] workspace (K contiguous) so both fragments are single 16-byte loads per lane
+// (probe: tools/microbench/mfma_i8_probe.hip; any k order shared by A and B is valid).
+constexpr int MK = 512;   // K of the W-CRT GEMM
+
+using v4i = int __attribute__((ext_vector_type(4)));
+using v16i = int __attribute__((ext_vector_type(16)));
+
+// one thread: column p (of Ppad; zero past P), 16 consecutive k; B (k, p) via the (sbK, sbY, log_n) map
+template <int D>
+__global__ __launch_bounds__(256) void mfma_digitize_kernel(const uint64_t* __restrict__ B, uint64_t bL,
+                                                            uint64_t sbK, uint64_t sbY, int log_n, uint32_t P,
+                                                            uint32_t Ppad, int8_t* __restrict__ out) {
+    const uint32_t p = blockIdx.x * 256 + threadIdx.x;
+    const int k0 = blockIdx.y * 16;
+    const int l = blockIdx.z;
+    if (p >= Ppad) return;
+    int8_t dig[D][16];
+    const uint64_t* Bl = B + (uint64_t)l * bL;
+    const uint64_t col = (uint64_t)(p >> log_n) * sbY + (p & ((1u << log_n) - 1));
+#pragma unroll
+    for (int kk = 0; kk < 16; ++kk) {
+        uint64_t x = p < P ? Bl[(uint64_t)(k0 + kk) * sbK + col] : 0;
+#pragma unroll
+        for (int i = 0; i < D; ++i) {
+            int v = (int)(x & 255);
+            x >>= 8;
+            if (v >= 128) {
+                v -= 256;
+                ++x;
+            }
+            dig[i][kk] = (int8_t)v;
+        }
+    }
+#pragma unroll
+    for (int i = 0; i < D; ++i) {
+        v4i v;
+        __builtin_memcpy(&v, dig[i], 16);
+        *(v4i*)(out + ((((uint64_t)l * D + i) * Ppad + p) * MK + k0)) = v;
+    }
+}
+
+template <int D>
+__global__ __launch_bounds__(256) void mod_gemm_mfma_kernel(ModGemmArgs a, uint32_t Ppad) {
+    constexpr int NS = 2 * D - 1;
+    const int l = blockIdx.z;
+    const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+    const int r = lane & 31, h = lane >> 5;
+    const int m0 = blockIdx.y * 64 + (w & 1) * 32;
+    const uint32_t p0 = blockIdx.x * 64 + (w >> 1) * 32;
+    const int8_t* Al = a.Adig + (uint64_t)l * a.adL;
+    const int8_t* Bl = a.Bdig + (uint64_t)l * D * Ppad * MK;
+    v16i acc[NS];
+#pragma unroll
+    for (int s = 0; s < NS; ++s) acc[s] = v16i{0};
+    for (int kc = 0; kc < MK / 32; ++kc) {
+        v4i av[D], bv[D];
+#pragma unroll
+        for (int i = 0; i < D; ++i) {
+            av[i] = *(const v4i*)(Al + ((uint64_t)i * 512 + m0 + r) * MK + kc * 32 + 16 * h);
+            bv[i] = *(const v4i*)(Bl + ((uint64_t)i * Ppad + p0 + r) * MK + kc * 32 + 16 * h);
+        }
+#pragma unroll
+        for (int i = 0; i < D; ++i)
+#pragma unroll
+            for (int j = 0; j < D; ++j) acc[i + j] = __builtin_amdgcn_mfma_i32_32x32x32_i8(av[i], bv[j], acc[i + j], 0, 0, 0);
+    }
+    // epilogue: C = sum_s acc_s * 256^s mod q
+    const uint64_t q = a.qmu[2 * l], mu = a.qmu[2 * l + 1];
+    const uint64_t* rt = a.rtab + (uint64_t)l * NS * 2;
+    uint64_t* C = a.C + (uint64_t)l * a.cL;
+    const uint32_t col = p0 + r;
+    if (col >= a.P) return;
+#pragma unroll
+    for (int reg = 0; reg < 16; ++reg) {
+        const int row = m0 + (reg & 3) + 8 * (reg >> 2) + 4 * h;
+        uint64_t sum = 0;
+#pragma unroll
+        for (int s = 0; s < NS; ++s) {
+            const int64_t v = acc[s][reg];
+            const uint64_t x = v < 0 ? (uint64_t)(v + (int64_t)q) : (uint64_t)v;   // |v| < 2^26 < q
+            uint64_t t = x * rt[2 * s] - __umul64hi(x, rt[2 * s + 1]) * q;        // Shoup: [0, 2q)
+            sum += t;                                                              // < 2 NS q < 2^64
+        }
+        uint64_t red = sum - __umul64hi(sum, mu) * q;   // Barrett: [0, 2q)
+        red = red >= q ? red - q : red;
+        C[(uint64_t)row * a.scM + (uint64_t)(col >> a.log_n) * a.scY + (col & ((1u << a.log_n) - 1))] = red;
+    }
+}
+
+size_t mod_gemm_mfma_ws(uint32_t P, int L, int D) {
+    const uint64_t Ppad = ((uint64_t)P + 63) / 64 * 64;
+    return (size_t)L * D * Ppad * MK;
+}
+
+void balanced_digits(uint64_t x, int D, int8_t* out) {
+    for (int i = 0; i < D; ++i) {
+        int v = (int)(x & 255);
+        x >>= 8;
+        if (v >= 128) {
+            v -= 256;
+            ++x;
+        }
+        out[i] = (int8_t)v;
+    }
+}
+
 int launch_mod_gemm(const ModGemmArgs& a, int L, hipStream_t s) {
+    if (a.Adig && a.M == 512 && a.K == MK) {
+        const uint32_t Ppad = (a.P + 63) / 64 * 64;
+        const dim3 gd((Ppad + 255) / 256, MK / 16, L), grid(Ppad / 64, 512 / 64, L);
+        switch (a.D) {
+#define MFHE_MFMA_CASE(d)                                                                                        \
+    case d:                                                                                                      \
+        hipLaunchKernelGGL(mfma_digitize_kernel<d>, gd, dim3(256), 0, s, a.B, a.bL, a.sbK, a.sbY, a.log_n, a.P,   \
+                           Ppad, a.Bdig);                                                                        \
+        hipLaunchKernelGGL(mod_gemm_mfma_kernel<d>, grid, dim3(256), 0, s, a, Ppad);                             \
+        break;
+            MFHE_MFMA_CASE(5)
+            MFHE_MFMA_CASE(6)
+            MFHE_MFMA_CASE(7)
+            MFHE_MFMA_CASE(8)
+#undef MFHE_MFMA_CASE
+            default: return set_error(MFHE_EINVAL, "mod_gemm: MFMA digit count must be 5..8");
+        }
+        MFHE_CHECK_LAUNCH("mod_gemm_mfma_kernel");
+        return MFHE_OK;
+    }
     dim3 grid((a.P + TP - 1) / TP, (a.M + TM - 1) / TM, L);
     hipLaunchKernelGGL(mod_gemm_kernel, grid, dim3(NTH), 0, s, a);
     MFHE_CHECK_LAUNCH("mod_gemm_kernel");

@@ -26,7 +26,20 @@ struct ModGemmArgs {
     uint32_t P;
     const uint64_t* qmu;   // [L][2] (q, floor(2^64/q))
     const uint64_t* r64;   // [L] 2^64 mod q
+    // i8 MFMA path (M = K = 512): A pre-split into D balanced base-256 digit planes [L][D][M][K] (limb
+    // stride adL bytes), rtab [L][2D-1][2] = (256^s mod q, Shoup), Bdig workspace >= L*D*Ppad*K bytes.
+    // Adig == nullptr selects the VALU u128 kernel.
+    const int8_t* Adig = nullptr;
+    uint64_t adL = 0;
+    int D = 0;
+    const uint64_t* rtab = nullptr;
+    int8_t* Bdig = nullptr;
 };
+
+// bytes of B digit workspace the MFMA path needs for P columns and L limbs at D digits
+size_t mod_gemm_mfma_ws(uint32_t P, int L, int D);
+// host: balanced base-256 digits of x (< 2^(8D-1)), D in [1, 8]
+void balanced_digits(uint64_t x, int D, int8_t* out);
 
 struct CGemmArgs {
     const double2* A;      // batch b at A + b*aB, row-major [M][K] (lda = K)

@@ -265,7 +265,28 @@ struct Bump {
 
 // W-CRT forward: B matrix-major [r][L][pos] (or vector [r][L][x]); C in the requested layout
 enum class WOut { Poly, Matrix, Vector };
-static int wcrt_gemm(const mfhe_ctx* c, const uint64_t* A, const uint64_t* B, bool b_poly, uint64_t* C, WOut out,
+#define RC(x) do { int _r = (x); if (_r) return _r; } while (0)
+
+// i8 MFMA operands for A = V or V^-1 (gemm.hip); leaves a on the VALU kernel when unavailable
+static int use_mfma(mfhe_ctx* c, ModGemmArgs& a, const uint64_t* A, int L) {
+    if (!c->wcrt_mfma || !c->wD || (A != c->d_wV && A != c->d_wVinv)) return MFHE_OK;
+    const size_t need = mod_gemm_mfma_ws(a.P, L, c->wD);
+    if (c->gemm_ws_bytes < need) {
+        if (c->gemm_ws) MFHE_HIP(hipFree(c->gemm_ws));
+        c->gemm_ws = nullptr;
+        c->gemm_ws_bytes = 0;
+        MFHE_HIP(hipMalloc(&c->gemm_ws, need));
+        c->gemm_ws_bytes = need;
+    }
+    a.Adig = A == c->d_wV ? c->d_wVdig : c->d_wVidig;
+    a.adL = a.aL ? (uint64_t)c->wD * 512 * 512 : 0;
+    a.D = c->wD;
+    a.rtab = c->d_wrtab;
+    a.Bdig = (int8_t*)c->gemm_ws;
+    return MFHE_OK;
+}
+
+static int wcrt_gemm(mfhe_ctx* c, const uint64_t* A, const uint64_t* B, bool b_poly, uint64_t* C, WOut out,
                      bool vector, hipStream_t s) {
     const Geo2 g = geo(c);
     ModGemmArgs a;
@@ -289,6 +310,7 @@ static int wcrt_gemm(const mfhe_ctx* c, const uint64_t* A, const uint64_t* B, bo
         if (out == WOut::Poly) { a.cL = g.n; a.scM = g.n * g.L * g.n; a.scY = (uint64_t)g.L * g.n; }
         else { a.cL = g.n2; a.scM = (uint64_t)g.L * g.n2; a.scY = g.n; }
     }
+    RC(use_mfma(c, a, A, g.L));
     return launch_mod_gemm(a, g.L, s);
 }
 
@@ -329,7 +351,6 @@ static int layout(const mfhe_ctx* c, const uint64_t* in, uint64_t* out, bool to_
     return MFHE_OK;
 }
 
-#define RC(x) do { int _r = (x); if (_r) return _r; } while (0)
 
 static int encode_impl(mfhe_ctx* c, const double* msg, uint64_t* out_re, uint64_t* out_im, hipStream_t s) {
     RC(need_wcrt(c));
@@ -516,6 +537,7 @@ extern "C" int mfhe_wcrt_inv_centered(mfhe_ctx* c, const int64_t* in, int64_t* o
     a.A = c->d_wVinv; a.aL = 0; a.M = a.K = 512; a.qmu = c->d_rns_mu; a.r64 = c->d_r64;
     a.B = rns; a.bL = 0; a.sbK = g.n2; a.sbY = g.n; a.log_n = g.logn; a.P = (uint32_t)g.n2;
     a.C = co; a.cL = 0; a.scM = g.n2; a.scY = g.n;
+    RC(use_mfma(c, a, c->d_wVinv, 1));
     RC(launch_mod_gemm(a, 1, s));
     hipLaunchKernelGGL(center_limb0_kernel, g1(g.cnt), dim3(256), 0, s, co, out, c->moduli[0], g.cnt);
     MFHE_CHECK_LAUNCH("center_limb0_kernel");

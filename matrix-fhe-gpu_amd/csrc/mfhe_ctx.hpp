@@ -67,6 +67,13 @@ struct mfhe_ctx {
     int ntt_fused = 0;       // N = 2^15..2^17: both passes in one launch (MFHE_OPT_NTT_FUSED)
     int ntt_fused_lag = 2;   // pass-2 lag in polynomials per XCD queue
     void* fused_buf = nullptr;   // FusedSync + map/arr arrays, grown on demand
+    int8_t* d_wVdig = nullptr;   // [L][wD][512][512] balanced base-256 digits of V   (i8 MFMA W-CRT)
+    int8_t* d_wVidig = nullptr;  // same for V^-1
+    uint64_t* d_wrtab = nullptr; // [L][2 wD - 1][2] (256^s mod q, Shoup)
+    int wD = 0;                  // 0: no MFMA tables (some q <= 2^27)
+    int wcrt_mfma = 1;           // MFHE_OPT_WCRT_MFMA
+    void* gemm_ws = nullptr;     // B digit planes for the MFMA GEMM, grown on demand
+    size_t gemm_ws_bytes = 0;
     size_t fused_bytes = 0;
 
     mfhe::LimbConst* d_limbs = nullptr;  // [L]

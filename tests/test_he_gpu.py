@@ -382,3 +382,38 @@ def test_kat7_kat8_encrypt_decrypt_reference_geometry(mfhe, pattern, tol):
     torch.cuda.synchronize()
     err = np.max(np.abs(out.cpu().numpy().view(np.complex128) - msg))
     assert err < tol, err
+
+
+@pytest.mark.parametrize("n,L", [(8, 11), (64, 11), (4, 2), (16, 1)])
+def test_wcrt_mfma_matches_valu_and_oracle(mfhe, orc, n, L):
+    """W-CRT GEMM on i8 MFMA (digit-split exact product, gemm.hip) == the u128 VALU kernel == oracle,
+    all three layouts (matrix->poly, poly->matrix, vector), bit-exact."""
+    import torch
+    log_n = n.bit_length() - 1
+    ctx = mfhe.Context(RNS[:L], log_n, CONV)
+    assert ctx.get_option(mfhe.OPT_WCRT_MFMA) == 1
+    rng = np.random.default_rng(n * 100 + L)
+    x = _rand_mat(rng, n, L)
+    outs = {}
+    for mf in (1, 0):
+        ctx.set_option(mfhe.OPT_WCRT_MFMA, mf)
+        d = _dev(mfhe, x)
+        f = torch.empty_like(d)
+        ctx.wcrt_fwd(d, f)
+        b = torch.empty_like(d)
+        ctx.wcrt_inv(f, b)
+        v = (rng.integers(0, 2 ** 63, (512, L, n), dtype=np.uint64) % np.array(RNS[:L], np.uint64)[None, :, None]).ravel()
+        vo = torch.empty(v.size, dtype=torch.int64, device="cuda")
+        ctx.wcrt_fwd_vector(_dev(mfhe, v), vo)
+        torch.cuda.synchronize()
+        outs[mf] = (mfhe.to_host_u64(f), mfhe.to_host_u64(b), mfhe.to_host_u64(vo))
+        np.testing.assert_array_equal(outs[mf][1], x)
+        rng = np.random.default_rng(n * 100 + L)   # same vector input for both runs
+        _rand_mat(rng, n, L)
+    for a, b in zip(outs[1], outs[0]):
+        np.testing.assert_array_equal(a, b)
+    if n <= 8:
+        h = orc.HE(n, RNS[:L], 2.0 ** 35)
+        ref = np.zeros_like(x)
+        orc.L.orc_wntt_forward_matrix(P(x), P(ref), n, L, 512, P(U64(RNS[:L])), orc.L.orc_he_V(h.h))
+        np.testing.assert_array_equal(outs[1][0], ref)
