@@ -15,12 +15,15 @@
 // those were pulled by running workgroups that never wait on later tasks.  Every spin is bounded;
 // a timeout sets FusedSync::err (read by mfhe_ctx_get_option(MFHE_OPT_NTT_FUSED_ERRORS)).
 //
-// Visibility (placement independent, MI355X_MICROARCH.md "inter-workgroup visibility"): producer
-// plain stores -> every wave s_waitcnt vmcnt(0) -> barrier -> lane 0 fence(release, agent) ->
-// s_waitcnt vmcnt(0) -> relaxed agent atomic add on the poly's arrival counter; consumer lane 0
-// polls the counter with relaxed agent loads -> fence(acquire, agent) -> s_waitcnt vmcnt(0) ->
-// barrier -> plain loads.  The release writes the XCD's dirty L2 lines back but keeps them resident,
-// so the same-XCD consumer still reads them from L2.
+// Visibility.  Producer and consumer of a hand-off always sit on the same XCD (the queue is chosen by
+// HW_REG_XCC_ID, never by blockIdx), so the XCD's L2 is the coherence point between them and the
+// intermediate never has to leave it (MI355X_MICROARCH.md "inter-workgroup visibility": stores keep
+// their lines in the XCD L2; only the CU's own L1 can be stale).  Producer: plain stores -> every wave
+// s_waitcnt vmcnt(0) (stores acknowledged by the L2) -> barrier -> lane 0 relaxed agent atomic add on the
+// poly's arrival counter.  Consumer: lane 0 polls the counter with sc1 (L1-bypass) loads -> barrier ->
+// every load of the intermediate is an sc1 load, served by the L2, so no L1 line of this CU (e.g. the
+// original input it read in pass 1) can be returned.  No agent release/acquire fence is needed: the
+// release's L2 write-back (buffer_wbl2) is exactly the traffic this kernel exists to avoid.
 #pragma once
 #include "ntt_kernels.hpp"
 
@@ -41,7 +44,7 @@ struct FusedSync {
 
 template <class TS>
 struct FusedArgs {
-    PassArgs<TS> p1, p2;   // pass 1 / pass 2 (forward: column then block; inverse: block then column)
+    PassArgs<TS> p;        // shared by pass 1 and pass 2 (forward: column then block; inverse: block then column)
     FusedSync* sync;
     uint64_t* map;
     uint32_t* arr;
@@ -76,8 +79,8 @@ __global__ __launch_bounds__(P1::NT) void ntt_fused_kernel(FusedArgs<TS> f) {
     const uint32_t x = xcc_id();
     FusedSync* sy = f.sync;
     const uint32_t K = f.K, D = f.lag;
-    const P1 p1(f.p1);
-    const P2 p2(f.p2);
+    const P1 p1(f.p);
+    const P2 p2(f.p);
 
     while (true) {
         __syncthreads();   // previous task's readers of bc[] are done
@@ -128,8 +131,6 @@ __global__ __launch_bounds__(P1::NT) void ntt_fused_kernel(FusedArgs<TS> f) {
                         __builtin_amdgcn_s_sleep(1);
                         if (++n == kSpinLimit) { atomicOr(&sy->err, 2u); break; }
                     }
-                    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
-                    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
                     kind = 2;
                 }
             }
@@ -138,7 +139,10 @@ __global__ __launch_bounds__(P1::NT) void ntt_fused_kernel(FusedArgs<TS> f) {
             bc[2] = j;
         }
         __syncthreads();
-        const uint32_t kind = bc[0], lb = bc[1], j = bc[2];
+        // readfirstlane: the broadcast words are workgroup-uniform, so tile addressing stays in SGPRs
+        const uint32_t kind = __builtin_amdgcn_readfirstlane(bc[0]);
+        const uint32_t lb = __builtin_amdgcn_readfirstlane(bc[1]);
+        const uint32_t j = __builtin_amdgcn_readfirstlane(bc[2]);
         if (kind == 3) break;
         if (kind == 0) continue;
         if (kind == 1) {
@@ -149,14 +153,12 @@ __global__ __launch_bounds__(P1::NT) void ntt_fused_kernel(FusedArgs<TS> f) {
             asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
             __syncthreads();
             if (t == 0) {
-                __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
-                asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
                 __hip_atomic_fetch_add(&f.arr[(size_t)x * f.cap + j], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
             }
         } else {
             const TileLoc L = p2.locate(lb);
             uint64_t raw[P2::R];
-            p2.load(L, raw);
+            p2.load_l2(L, raw);
             p2.compute_store(L, raw, lds);
         }
     }

@@ -159,21 +159,34 @@ struct NttPass {
 
     const PassArgs<TS>& a;
     uint32_t gl, tau;
-    int logS;
+    int s0, logS;   // a column pass is always the first LOG_G stages, a block pass the last LOG_G
 
     __device__ __forceinline__ explicit NttPass(const PassArgs<TS>& args) : a(args) {
         const uint32_t t = threadIdx.x;
         gl = COLS ? (t % NG) : (t / TG);
         tau = COLS ? (t / NG) : (t % TG);
-        logS = a.logN - a.s0 - LOG_G;
+        s0 = COLS ? 0 : a.logN - LOG_G;
+        logS = a.logN - s0 - LOG_G;
     }
     __device__ __forceinline__ uint32_t jidx(const TileLoc& L, uint32_t g) const { return L.off0 | (g << logS); }
     __device__ __forceinline__ TileLoc locate(uint32_t lb) const {
-        return tile_loc<LOG_G, NG, COLS, UNI>(a.data, a.batch, a.nl, a.start_limb, a.logN, a.s0, lb, gl);
+        return tile_loc<LOG_G, NG, COLS, UNI>(a.data, a.batch, a.nl, a.start_limb, a.logN, s0, lb, gl);
     }
     __device__ __forceinline__ void load(const TileLoc& L, uint64_t (&raw)[R]) const {
 #pragma unroll
         for (int k = 0; k < R; ++k) raw[k] = L.base[jidx(L, Gm::g_of(r_load, tau, k))];
+    }
+
+    // L1-bypass (sc1) loads, served by the XCD's L2: reads data another CU of this XCD just stored.
+    // Buffer loads off the workgroup-uniform tile base (UNI plans): SGPR descriptor + 32-bit lane offset.
+    __device__ __forceinline__ void load_l2(const TileLoc& L, uint64_t (&raw)[R]) const {
+        static_assert(UNI, "load_l2 needs a workgroup-uniform tile base");
+        constexpr int kSc1 = 16;   // CPol::SC1 (gfx940+ cache-policy bits)
+        const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(L.base, 0, 0x7FFFFFFF, 0x00020000);
+#pragma unroll
+        for (int k = 0; k < R; ++k)
+            raw[k] = __builtin_bit_cast(uint64_t, __builtin_amdgcn_raw_buffer_load_b64(
+                                                      rs, (int)(jidx(L, Gm::g_of(r_load, tau, k)) * 8u), 0, kSc1));
     }
 
     __device__ __forceinline__ void compute_store(const TileLoc& L, const uint64_t (&raw)[R], uint64_t* lds) const {
@@ -220,7 +233,7 @@ struct NttPass {
             constexpr int hb = Gm::HB(r), wl = Gm::WL(r);
             constexpr int bit = wl + bb;
             if constexpr (bit <= hb) {
-                const int s = a.s0 + (LOG_G - 1 - bit);
+                const int s = s0 + (LOG_G - 1 - bit);
                 constexpr int half = 1 << bb;
                 const uint64_t tau_hi = tau_ >> wl;
                 const uint64_t twb =
@@ -330,9 +343,18 @@ __device__ __forceinline__ void pass_loop(const PassArgs<TS>& a, uint64_t* lds) 
     }
 }
 
+// Minimum resident workgroups per CU the register allocation must allow (launch-bounds waves/SIMD).
+#ifndef MFHE_NTT_MIN_WG_CU
+#define MFHE_NTT_MIN_WG_CU 1
+#endif
+constexpr int min_waves_per_simd(int nt) {
+    return (MFHE_NTT_MIN_WG_CU * nt / 256) < 1 ? 1 : (MFHE_NTT_MIN_WG_CU * nt / 256);
+}
+
 template <class A, class TS, int LOG_G, int LOG_R, int NG, bool COLS, bool INV, bool IN_RAW, bool OUT_RAW,
           bool TWIST, bool BREV, bool UNI, bool PF>
-__global__ __launch_bounds__(NG * (1 << (LOG_G - LOG_R))) void ntt_pass_kernel(PassArgs<TS> a) {
+__global__ __launch_bounds__(NG * (1 << (LOG_G - LOG_R)), min_waves_per_simd(NG * (1 << (LOG_G - LOG_R))))
+void ntt_pass_kernel(PassArgs<TS> a) {
     extern __shared__ __attribute__((aligned(16))) uint64_t lds[];
     pass_loop<NttPass<A, TS, LOG_G, LOG_R, NG, COLS, INV, IN_RAW, OUT_RAW, TWIST, BREV, UNI>, PF>(a, lds);
 }

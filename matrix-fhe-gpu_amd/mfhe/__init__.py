@@ -16,7 +16,8 @@ from pathlib import Path
 
 _PKG_DIR = Path(__file__).resolve().parent.parent          # matrix-fhe-gpu_amd/
 REPO_ROOT = _PKG_DIR.parent
-LIB_PATH = _PKG_DIR / "libmfhe.so"
+# MFHE_LIB: load a tuning-variant build instead (tools only; the product path is libmfhe.so)
+LIB_PATH = Path(os.environ["MFHE_LIB"]) if os.environ.get("MFHE_LIB") else _PKG_DIR / "libmfhe.so"
 HEADER = REPO_ROOT / "include" / "mfhe.h"
 
 OK, EINVAL, EUNSUPPORTED, EHIP, ENOMEM, ENOTREADY = 0, 1, 2, 3, 4, 5
