@@ -141,6 +141,82 @@ __device__ __forceinline__ void compose_slow(const uint64_t* __restrict__ in, ui
     }
 }
 
+// FP64 small-value fast path (every q < 2^50 and odd; ctx table CrtLimbF).  Same acceptance rule as the
+// integer fast path below, cheaper arithmetic: t_k = x_k * inv_k mod q_k comes from one FP64 error-free
+// product as an exact integer in (-q, q) -- not canonicalised: any representative of the class gives the
+// same CRT value -- est = sum_k t_k / q_k, u = rint(est), c = low64(sum_k t_k M_k - u Q) in wrapping
+// int64.  c is accepted iff |c| < 2^62, |c| <= Q_half and q_k | (c - x_k) for every k, tested exactly
+// as |c - x_k| * q_k^-1 mod 2^64 <= floor((2^64-1)/q_k) (q_k odd); by CRT uniqueness c is then THE
+// centred value, bit-identical to compose_slow.  Residues are loaded CH limbs at a time so each thread
+// has CH loads in flight; for L <= CH the divisibility pass reuses the registers.
+template <int CH>
+__device__ __forceinline__ bool compose_fast_f64(const uint64_t* __restrict__ in, uint64_t ncoeff, int L, int Lg,
+                                                 uint64_t shard_stride, const CrtLimbF* __restrict__ lf,
+                                                 uint64_t Q0, uint64_t Qh0, bool qbig, uint64_t& mag0, bool& neg) {
+    constexpr double kMagic = 6755399441055744.0;   // 1.5 * 2^52
+    const int64_t kMagicBits = __double_as_longlong(kMagic);
+    uint64_t xs[CH];
+    double est = 0.0;
+    uint64_t lo = 0;
+    const uint64_t* p = in;
+    int j = 0;
+    for (int k0 = 0; k0 < L; k0 += CH) {
+#pragma unroll
+        for (int i = 0; i < CH; ++i) {
+            if (k0 + i < L) {
+                xs[i] = p[(uint64_t)j * ncoeff];
+                if (++j == Lg) {
+                    j = 0;
+                    p += shard_stride;
+                }
+            }
+        }
+#pragma unroll
+        for (int i = 0; i < CH; ++i) {
+            if (k0 + i < L) {
+                const CrtLimbF f = lf[k0 + i];
+                const double xv = __longlong_as_double((long long)(xs[i] | 0x4330000000000000ULL)) - 4503599627370496.0;
+                const double hi = xv * f.invf;
+                const double elo = __fma_rn(xv, f.invf, -hi);
+                const double kq = __fma_rn(hi, f.qinvf, kMagic) - kMagic;
+                const double t = __fma_rn(-kq, f.qf, hi) + elo;       // exact, |t| < q
+                est = __fma_rn(t, f.qinvf, est);
+                const int64_t ti = __double_as_longlong(t + kMagic) - kMagicBits;
+                lo += (uint64_t)ti * f.M0;                               // wrapping
+            }
+        }
+    }
+    const int64_t u = (int64_t)__builtin_rint(est);
+    const int64_t c = (int64_t)(lo - (uint64_t)u * Q0);
+    const uint64_t a = c < 0 ? (uint64_t)0 - (uint64_t)c : (uint64_t)c;
+    bool ok = a < (1ull << 62) && (qbig || a <= Qh0);
+    auto divides = [&](uint64_t x, const CrtLimbF& f) {
+        const int64_t d = c - (int64_t)x;
+        const uint64_t ad = d < 0 ? (uint64_t)0 - (uint64_t)d : (uint64_t)d;
+        return ad * f.qinv64 <= f.lim;
+    };
+    if (ok) {
+        if (L <= CH) {
+#pragma unroll
+            for (int i = 0; i < CH; ++i)
+                if (i < L) ok &= divides(xs[i], lf[i]);
+        } else {
+            p = in;
+            j = 0;
+            for (int k = 0; k < L && ok; ++k) {
+                ok = divides(p[(uint64_t)j * ncoeff], lf[k]);
+                if (++j == Lg) {
+                    j = 0;
+                    p += shard_stride;
+                }
+            }
+        }
+    }
+    mag0 = a;
+    neg = c < 0;
+    return ok;
+}
+
 // Small-value fast path.  With u = nearest integer to sum_k t_k/q_k, the centred CRT value is
 // X = sum_k t_k M_k - u Q; its low 64 bits cost one wrapping multiply-add per limb.  The candidate
 // c = (int64) low64(X) is accepted only if |c| <= Q_half and c = x_k (mod q_k) for every k: by CRT
@@ -152,7 +228,19 @@ __device__ __forceinline__ void compose_one(const uint64_t* __restrict__ in, uin
                                             uint64_t shard_stride, const uint64_t* __restrict__ qmu,
                                             const uint64_t* __restrict__ inv, const double* __restrict__ qinv,
                                             const uint64_t* __restrict__ M, const uint64_t* __restrict__ Q,
-                                            const uint64_t* __restrict__ Qh, uint64_t (&mag)[W], bool& neg) {
+                                            const uint64_t* __restrict__ Qh, uint64_t (&mag)[W], bool& neg,
+                                            const CrtLimbF* __restrict__ lf, bool qbig) {
+    if (lf) {
+        uint64_t a0;
+        if (compose_fast_f64<8>(in, ncoeff, L, Lg, shard_stride, lf, Q[0], Qh[0], qbig, a0, neg)) {
+            mag[0] = a0;
+#pragma unroll
+            for (int i = 1; i < W; ++i) mag[i] = 0;
+            return;
+        }
+        compose_slow<W>(in, ncoeff, L, Lg, shard_stride, qmu, inv, qinv, M, Q, Qh, mag, neg);
+        return;
+    }
     uint64_t lo = 0;
     double est = 0.0;
     {
@@ -173,9 +261,6 @@ __device__ __forceinline__ void compose_one(const uint64_t* __restrict__ in, uin
     const uint64_t u = (uint64_t)__builtin_rint(est);
     const int64_t c = (int64_t)(lo - u * Q[0]);
     const uint64_t a = c < 0 ? (uint64_t)0 - (uint64_t)c : (uint64_t)c;
-    bool qbig = false;   // Q_half >= 2^64: every |c| < 2^62 is inside (-Q/2, Q/2)
-#pragma unroll
-    for (int i = 1; i < W; ++i) qbig |= Qh[i] != 0;
     bool ok = a < (1ull << 62) && (qbig || a <= Qh[0]);
     {
         const uint64_t* p = in;
@@ -220,6 +305,8 @@ struct CrtArgs {
     const uint64_t *qmu, *inv;
     const double* qinv;
     const uint64_t *M, *Q, *Qh;
+    const CrtLimbF* lf;       // FP64 fast-path constants (null: integer fast path)
+    bool qbig;                // Q_half >= 2^64: every |c| < 2^62 is inside (-Q/2, Q/2)
 };
 
 template <int W>
@@ -231,7 +318,7 @@ __global__ __launch_bounds__(256) void crt_compose_kernel(CrtArgs a, uint64_t* _
     uint64_t mag[W];
     bool neg;
     compose_one<W>(a.in + p * (uint64_t)a.Lg * a.ncoeff + c, a.ncoeff, a.L, a.Lg, a.shard_stride, a.qmu, a.inv,
-                   a.qinv, a.M, a.Q, a.Qh, mag, neg);
+                   a.qinv, a.M, a.Q, a.Qh, mag, neg, a.lf, a.qbig);
     uint64_t* o = out_mag + i * W;
 #pragma unroll
     for (int w = 0; w < W; ++w) o[w] = mag[w];
@@ -247,7 +334,7 @@ __global__ __launch_bounds__(256) void crt_compose_f64_kernel(CrtArgs a, double 
     uint64_t mag[W];
     bool neg;
     compose_one<W>(a.in + p * (uint64_t)a.Lg * a.ncoeff + c, a.ncoeff, a.L, a.Lg, a.shard_stride, a.qmu, a.inv,
-                   a.qinv, a.M, a.Q, a.Qh, mag, neg);
+                   a.qinv, a.M, a.Q, a.Qh, mag, neg, a.lf, a.qbig);
     out[i * out_stride] = big_to_f64<W>(mag, neg, delta);
 }
 
@@ -281,6 +368,8 @@ static CrtArgs crt_args(const mfhe_ctx* c, const uint64_t* in, uint64_t npoly, u
     a.M = c->d_crt_M;
     a.Q = c->d_crt_Q;
     a.Qh = c->d_crt_Qhalf;
+    a.lf = c->d_crt_lf;
+    a.qbig = c->crt_qbig;
     return a;
 }
 

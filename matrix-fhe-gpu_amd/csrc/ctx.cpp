@@ -162,6 +162,19 @@ static int build_crt(mfhe_ctx* c, int min_words) {
         r64[k] = (uint64_t)((((hm::u128)1) << 64) % q);
     }
     int rc;
+    c->crt_qbig = std::any_of(Qh.begin() + 1, Qh.end(), [](uint64_t w) { return w != 0; });
+    // FP64 fast-path constants: every q < 2^50 (exact FP64 mulmod) and odd (divisibility test)
+    c->d_crt_lf = nullptr;
+    if (c->f64_ok && std::all_of(c->moduli.begin(), c->moduli.end(), [](uint64_t q) { return (q & 1) != 0; })) {
+        std::vector<CrtLimbF> lf(L);
+        for (int k = 0; k < L; ++k) {
+            const uint64_t q = c->moduli[k];
+            uint64_t qi = q;   // Newton: q^-1 mod 2^64 (q odd), 5 steps from 3 correct bits
+            for (int it = 0; it < 5; ++it) qi *= 2 - q * qi;
+            lf[k] = CrtLimbF{q, (double)q, (double)inv[2 * k], qinv[k], M[(size_t)k * W], qi, ~0ull / q, 0};
+        }
+        if ((rc = upload(c, &c->d_crt_lf, lf))) return rc;
+    }
     if ((rc = upload(c, &c->d_crt_M, M)) || (rc = upload(c, &c->d_crt_inv, inv)) ||
         (rc = upload(c, &c->d_crt_qinv, qinv)) || (rc = upload(c, &c->d_crt_Q, Q)) ||
         (rc = upload(c, &c->d_crt_Qhalf, Qh)) || (rc = upload(c, &c->d_rns_mu, mu)) ||

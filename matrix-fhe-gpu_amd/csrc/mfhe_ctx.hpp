@@ -33,6 +33,16 @@ int ensure_xy(mfhe_ctx* c);   // XY encoder matrices, built on first use (ctx.cp
         if (_e != hipSuccess) return ::mfhe::hip_error(_e, what); \
     } while (0)
 
+// Per-limb constants of the FP64 wide-CRT fast path (crt.hip compose_fast): one 64-B scalar load per limb.
+struct CrtLimbF {
+    uint64_t q;
+    double qf, invf, qinvf;   // q, (M_k mod q)^-1, 1/q as doubles (exact: q < 2^50)
+    uint64_t M0;              // low word of M_k = Q / q_k
+    uint64_t qinv64;          // q^-1 mod 2^64 (q odd): exact-divisibility test
+    uint64_t lim;             // floor((2^64 - 1) / q)
+    uint64_t pad;
+};
+
 struct NttTablesF {   // FP64 path: centred w
     double* tw = nullptr;    // [L][N]
     double* itw = nullptr;   // [L][N], itw[1] *= n^-1
@@ -99,6 +109,8 @@ struct mfhe_ctx {
     uint64_t* d_crt_Qhalf = nullptr;  // [W]
     uint64_t* d_rns_mu = nullptr;     // [L][2] (q, floor(2^64/q))
     uint64_t* d_r64 = nullptr;        // [L]     2^64 mod q
+    bool crt_qbig = false;            // Q_half >= 2^64
+    mfhe::CrtLimbF* d_crt_lf = nullptr;  // [L] FP64 compose constants (null: some q >= 2^50 or even)
 
     // W axis (MFHE_CONV_WCRT), phi = 512
     static constexpr int PHI = 512;

@@ -105,16 +105,23 @@ def test_decompose_compose_roundtrip_full_size(mfhe):
     assert torch.equal(out, expect)
 
 
+@pytest.mark.parametrize("small", [False, True])
 @pytest.mark.parametrize("world", [2, 4, 8])
-def test_crt_compose_f64_sharded_matches_unsharded(mfhe, orc, world):
-    """mfhe_crt_compose_f64_sharded reads the all-gather / all-to-all receive layouts in place."""
+def test_crt_compose_f64_sharded_matches_unsharded(mfhe, orc, world, small):
+    """mfhe_crt_compose_f64_sharded reads the all-gather / all-to-all receive layouts in place, on random
+    residues (full multi-word path) and on residues of small centred values (FP64 fast path)."""
     import torch
     moduli = orc.gen_primes(50, 1 << 18, 16)
     ctx = mfhe.Context(moduli, 16, mfhe.CONV_PHANTOM)
     B, L, N = 2 * world, 16, 2048
     lg, bs = L // world, 2
     rng = np.random.default_rng(world)
-    full = rng.integers(0, 2 ** 63, (B, L, N), dtype=np.uint64) % np.array(moduli, np.uint64)[None, :, None]
+    qv = np.array(moduli, np.uint64)[None, :, None]
+    if small:
+        v = rng.integers(-(2 ** 61), 2 ** 61, (B, 1, N), dtype=np.int64)
+        full = np.where(v < 0, (qv - (np.abs(v).astype(np.uint64) % qv)) % qv, v.astype(np.uint64) % qv)
+    else:
+        full = rng.integers(0, 2 ** 63, (B, L, N), dtype=np.uint64) % qv
     ref = torch.empty(bs * N, dtype=torch.float64, device="cuda")
     got = torch.empty_like(ref)
     # all-gather layout: [world][B][lg][N]; rank r composes polys [r*bs, (r+1)*bs)
@@ -133,7 +140,7 @@ def test_crt_compose_f64_sharded_matches_unsharded(mfhe, orc, world):
         assert torch.equal(got, ref)
 
 
-@pytest.mark.parametrize("L,W", [(1, None), (1, 7), (2, None), (8, None), (11, 7)])
+@pytest.mark.parametrize("L,W", [(1, None), (1, 7), (2, None), (8, None), (9, None), (11, 7), (16, None), (32, None)])
 def test_crt_compose_small_value_fast_path_boundaries(mfhe, orc, L, W):
     """Centred values around the fast path's limits (|X| near 2^62, near Q/2 for small Q) must match the
     full multi-word compose bit-exactly (oracle), whichever path the kernel takes."""
