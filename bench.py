@@ -82,6 +82,23 @@ def is_prime(n):
     return True
 
 
+def pmc_traffic(N, L, batch):
+    """HBM-side bytes per forward transform from the committed rocprofv3 FETCH_SIZE/WRITE_SIZE passes
+    (tools/pmc_run.sh + tools/pmc_summary.py -> profiles/*pmc_ntt_traffic.json), if one was measured on
+    this exact shape; counters cannot be read from inside a timed run."""
+    import glob
+    best = None
+    for f in sorted(glob.glob(str(ROOT / "profiles" / "*pmc_ntt_traffic*.json"))):
+        try:
+            d = json.load(open(f))
+        except (OSError, ValueError):
+            continue
+        c = d.get("config", {})
+        if (c.get("N"), c.get("limbs"), c.get("batch")) == (N, L, batch) and "fwd_traffic_bytes_per_transform" in d:
+            best = (d["fwd_traffic_bytes_per_transform"], Path(f).name)
+    return best
+
+
 def cpu_baseline(log_n, moduli, seconds):
     """Reference CPU path restated (oracle, Harvey/Shoup phantom NTT, OpenMP over polys)."""
     import numpy as np
@@ -251,9 +268,15 @@ def main():
             out["roofline"] = {"bound": "hbm", "kernel": "mfhe_ntt_fwd (2 launches: column pass + block pass)",
                                "achieved": round(ach, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                                "frac": round(ach / HBM_PEAK_GBS, 4), "traffic": None,
+                               "traffic_unit": "bytes per transform (FETCH_SIZE x2 + WRITE_SIZE, L2<->fabric)",
                                "algorithmic_bytes_per_launch": alg_bytes,
                                "hbm_read_frac": round(ach / 2 / HBM_PEAK_GBS, 4),
                                "event_ms_per_transform": round(res["fwd_ev_ms"], 4)}
+            tr = pmc_traffic(N, L, batch)
+            if tr:
+                out["roofline"]["traffic"] = tr[0]
+                out["roofline"]["traffic_source"] = f"profiles/{tr[1]}"
+                out["roofline"]["traffic_over_algorithmic"] = round(tr[0] / alg_bytes, 3)
             out["inverse_NTT_per_s"] = batch * L / (res["inv_ev_ms"] * 1e-3) * world
         if "crt_ev_ms" in res:
             cb = res["crt_batch"]

@@ -79,6 +79,15 @@ struct ArithF64 {
         u = reduce(a + b);
         v = mulmod(a - b, w);
     }
+    // GS without reducing X: used on every other inverse stage.  Inputs of a lazy stage are outputs of a
+    // reduced stage (|x| <= 0.83 q: centred reduce or mulmod with a +-1 quotient) or canonical (< q), so
+    // its X outputs stay < 2q and the next (reducing) stage sees |u - v| < 4q: |(u - v) w / q| < 2^51
+    // with centred |w| <= q/2 and q < 2^50, inside mulmod's rounding range.
+    __device__ __forceinline__ void gs_lazy(double& u, double& v, Tw w) const {
+        double a = u, b = v;
+        u = a + b;
+        v = mulmod(a - b, w);
+    }
     // start-of-round reduction (keeps CT growth bounded)
     __device__ __forceinline__ double round_reduce(double x) const { return reduce(x); }
     // exact canonical u64 in [0, q)
@@ -120,6 +129,7 @@ struct ArithU64 {
         u = reduce(a + b);
         v = mulmod(a - b + two_q, w);
     }
+    __device__ __forceinline__ void gs_lazy(uint64_t& u, uint64_t& v, Tw w) const { gs(u, v, w); }
     __device__ __forceinline__ uint64_t round_reduce(uint64_t x) const { return x; }
     __device__ __forceinline__ uint64_t canon(uint64_t x) const {
         x = (x >= two_q) ? x - two_q : x;

@@ -246,6 +246,11 @@ struct NttPass {
                         ar.ct(x[k], x[k + half], w);
                     }
                 } else {
+                    // executed-stage index inside this pass (inverse rounds run r = NR-1 .. 0; only the first
+                    // round can skip stages, at its top bits): even -> lazy GS, odd -> reducing GS
+                    constexpr int ri = NR - 1 - r;
+                    constexpr int first = (Gm::HB(NR - 1) < LOG_R - 1 ? Gm::HB(NR - 1) : LOG_R - 1) + 1;
+                    constexpr int e = ri == 0 ? bb : first + (ri - 1) * LOG_R + bb;
                     if (s == 0) {
                         const Tw wn = a.ninv.get((size_t)L.mod);
                         const Tw w1 = a.tw.get(twoff + 1);
@@ -253,7 +258,7 @@ struct NttPass {
                         for (int k = 0; k < R; ++k) {
                             if (k & half) continue;
                             T u = x[k], vv = x[k + half];
-                            ar.gs(u, vv, w1);          // u = red(u+v), vv = (u-v) * itw[1]
+                            ar.gs_lazy(u, vv, w1);     // u = u+v, vv = (u-v) * itw[1]
                             x[k] = ar.mulmod(u, wn);   // X * n^-1
                             x[k + half] = vv;
                         }
@@ -262,7 +267,8 @@ struct NttPass {
                         for (int k = 0; k < R; ++k) {
                             if (k & half) continue;
                             const Tw w = a.tw.get(twb + (uint64_t)(k >> (bb + 1)));
-                            ar.gs(x[k], x[k + half], w);
+                            if constexpr (e % 2 == 0) ar.gs_lazy(x[k], x[k + half], w);
+                            else ar.gs(x[k], x[k + half], w);
                         }
                     }
                 }

@@ -42,7 +42,10 @@ def main():
         d = torch.randint(0, 2 ** 62, (batch * L * N,), dtype=torch.int64, device="cuda") % q
         ref = d.clone()
         chunks = [192 << 20, 0] if log_n > 14 else [192 << 20]
-        if log_n >= 15:
+        import os
+        if os.environ.get("CHUNKS"):
+            chunks = [int(x) << 20 for x in os.environ["CHUNKS"].split(",")]
+        if log_n >= 15 and not os.environ.get("NOFUSED"):
             for lag in (1, 2, 3, 4, 6):
                 ctx.set_option(OPT_FUSED, 1)
                 ctx.set_option(OPT_LAG, lag)
@@ -61,7 +64,7 @@ def main():
         import os
         quick = os.environ.get("QUICK") == "1"
         for pf in ((0,) if quick else (0, 1)):
-            for wg in ((0, 16) if quick else (0, 1, 2, 3, 4, 16)):
+            for wg in ((16,) if os.environ.get("WG16") else (0, 16) if quick else (0, 1, 2, 3, 4, 16)):
                 for cb in chunks:
                     ctx.set_option(OPT_PF, pf)
                     ctx.set_option(OPT_WG, wg)

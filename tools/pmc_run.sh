@@ -7,7 +7,7 @@ TAG=${1:-pmc}
 ROOT=${GRAFT_REPO_ROOT:-$(pwd)}
 OUT=$ROOT/gpurun_out/$TAG
 mkdir -p "$OUT"
-make -C "$ROOT/tools/microbench" -f /dev/null >/dev/null 2>&1
+[ -x "$ROOT/tools/microbench/pmc_calib" ] || { echo "build tools/microbench/pmc_calib first (hipcc, in this container)"; exit 2; }
 cd /tmp && export TMPDIR=/tmp
 for C in FETCH_SIZE WRITE_SIZE; do
   timeout -k 10 240 rocprofv3 --pmc $C -d "$OUT/calib_$C" -o run --output-format csv -- \
