@@ -94,18 +94,34 @@ __global__ void gaussian_kernel(uint64_t* e, const uint64_t* qmu, int L, int log
 }
 
 // ---------------- ring ops (poly-major [phi*n][L][n]) ----------------
-// pointwise_mul_s_kernel HE.cu:509-531: t = a * s[w][l][x], w = poly / n
-__global__ void mul_s_kernel(const uint64_t* a, const uint64_t* s, uint64_t* t, const uint64_t* qmu, int L, int log_n,
-                             uint64_t total) {
-    const uint64_t idx = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x;
+// pointwise_mul_s_kernel HE.cu:509-531: t = a * s[w][l][x], w = poly / n.  The reference reduces with
+// an __int128 % per element (a software division here too); this uses the exact FP64 modmul of the NTT
+// (ntt_arith.hpp) when every q < 2^50, else a u128 fold with 2^64 mod q and one Barrett step.
+__global__ __launch_bounds__(256) void mul_s_kernel(const uint64_t* __restrict__ a, const uint64_t* __restrict__ s,
+                                                    uint64_t* __restrict__ t, const uint64_t* __restrict__ qmu,
+                                                    const uint64_t* __restrict__ r64, const LimbConst* __restrict__ lf,
+                                                    int L, int log_n, uint32_t total) {
+    const uint32_t idx = blockIdx.x * blockDim.x + threadIdx.x;
     if (idx >= total) return;
-    const uint64_t n = 1ull << log_n, single = (uint64_t)L * n;
-    const uint64_t off = idx % single, poly = idx / single;
+    const uint32_t n = 1u << log_n, single = (uint32_t)L << log_n;
+    const uint32_t poly = idx / single, off = idx - poly * single;
     const int l = (int)(off >> log_n);
-    const uint64_t coeff = off & (n - 1), w = poly >> log_n;
-    const uint64_t q = qmu[2 * l];
-    const unsigned __int128 pr = (unsigned __int128)a[idx] * s[(w * L + l) * n + coeff];
-    t[idx] = (uint64_t)(pr % q);
+    const uint32_t coeff = off & (n - 1), w = poly >> log_n;
+    const uint64_t av = a[idx], sv = s[((uint64_t)w * L + l) * n + coeff];
+    if (lf) {
+        const ArithF64 ar(lf[l]);
+        t[idx] = ar.canon(ar.mulmod(ArithF64::from_u64(av), ArithF64::from_u64(sv)));
+        return;
+    }
+    const uint64_t q = qmu[2 * l], mu = qmu[2 * l + 1], rr = r64[l];
+    uint64_t hi = __umul64hi(av, sv), lo = av * sv;
+    while (hi) {
+        const unsigned __int128 f = (unsigned __int128)hi * rr + lo;
+        hi = (uint64_t)(f >> 64);
+        lo = (uint64_t)f;
+    }
+    uint64_t r = lo - __umul64hi(lo, mu) * q;
+    t[idx] = r >= q ? r - q : r;
 }
 
 // combine_b_kernel HE.cu:535-547 (b = m - t + e) and add_poly_kernel HE.cu:549-560 (b + t)
@@ -442,7 +458,9 @@ static int encrypt_impl(mfhe_ctx* c, const uint64_t* m_re, const uint64_t* m_im,
     RC(wcrt_gemm(c, c->d_wV, ep, false, eev, WOut::Poly, false, s));
     // t = INTT(a_ntt * s)  (reuse ep as t)
     uint64_t* t = ep;
-    hipLaunchKernelGGL(mul_s_kernel, g1(W), dim3(256), 0, s, ant, sk, t, c->d_rns_mu, g.L, g.logn, W);
+    if (W >= (1ull << 32)) return set_error(MFHE_EUNSUPPORTED, "ciphertext of 2^32 words or more");
+    hipLaunchKernelGGL(mul_s_kernel, g1(W), dim3(256), 0, s, ant, sk, t, c->d_rns_mu, c->d_r64,
+                       c->f64_ok ? c->d_limbs : nullptr, g.L, g.logn, (uint32_t)W);
     MFHE_CHECK_LAUNCH("mul_s_kernel");
     RC(mfhe_ntt_inv(c, t, 512 * g.n, 0, g.L, (mfhe_stream_t)s));
     const uint64_t* ms[2] = {m_re, m_im};
@@ -468,7 +486,9 @@ static int decrypt_impl(mfhe_ctx* c, const uint64_t* ct, const uint64_t* sk, uin
     RC(layout(c, ct, bp, true, s));
     RC(layout(c, ct + W, ap, true, s));
     RC(mfhe_ntt_fwd(c, ap, 512 * g.n, 0, g.L, (mfhe_stream_t)s));
-    hipLaunchKernelGGL(mul_s_kernel, g1(W), dim3(256), 0, s, ap, sk, t, c->d_rns_mu, g.L, g.logn, W);
+    if (W >= (1ull << 32)) return set_error(MFHE_EUNSUPPORTED, "ciphertext of 2^32 words or more");
+    hipLaunchKernelGGL(mul_s_kernel, g1(W), dim3(256), 0, s, ap, sk, t, c->d_rns_mu, c->d_r64,
+                       c->f64_ok ? c->d_limbs : nullptr, g.L, g.logn, (uint32_t)W);
     MFHE_CHECK_LAUNCH("mul_s_kernel");
     RC(mfhe_ntt_inv(c, t, 512 * g.n, 0, g.L, (mfhe_stream_t)s));
     hipLaunchKernelGGL(combine_kernel, g1(W), dim3(256), 0, s, bp, t, nullptr, out, c->d_rns_mu, g.L, g.logn, W, 1);
