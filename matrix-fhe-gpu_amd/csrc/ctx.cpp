@@ -277,6 +277,28 @@ static int build_wcrt(mfhe_ctx* c) {
         if ((rc = upload(c, &c->d_wVdig, vd)) || (rc = upload(c, &c->d_wVidig, vid)) || (rc = upload(c, &c->d_wrtab, rt)))
             return rc;
         c->wD = D;
+        // per-limb digit count: a value < q < 2^(8 d - 1) has zero balanced digits from d on, so limb l's
+        // products with those planes vanish and its GEMM runs at d_l^2 instead of D^2 MFMAs
+        c->wDl.resize(L);
+        for (int l = 0; l < L; ++l) {
+            const int b = 64 - __builtin_clzll(c->moduli[l]);
+            c->wDl[l] = std::min(D, std::max(1, (b + 1 + 7) / 8));
+        }
+        // FP64 epilogue constants (every q < 2^50): q, 1/q and centred 2^32, 2^64, 2^96 mod q
+        if (c->f64_ok) {
+            std::vector<double> ep((size_t)L * 8, 0.0);
+            for (int l = 0; l < L; ++l) {
+                const uint64_t q = c->moduli[l];
+                const uint64_t p32 = (uint64_t)((((hm::u128)1) << 32) % q);
+                const uint64_t p64 = hm::mulmod(p32, p32, q), p96 = hm::mulmod(p64, p32, q);
+                ep[(size_t)l * 8 + 0] = (double)q;
+                ep[(size_t)l * 8 + 1] = 1.0 / (double)q;
+                ep[(size_t)l * 8 + 2] = centred(p32, q);
+                ep[(size_t)l * 8 + 3] = centred(p64, q);
+                ep[(size_t)l * 8 + 4] = centred(p96, q);
+            }
+            if ((rc = upload(c, &c->d_wepi, ep))) return rc;
+        }
     }
     return MFHE_OK;
 }

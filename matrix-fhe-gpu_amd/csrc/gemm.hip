@@ -197,15 +197,15 @@ __global__ __launch_bounds__(256) void mfma_digitize_kernel(const uint64_t* __re
 }
 
 template <int D>
-__global__ __launch_bounds__(256) void mod_gemm_mfma_kernel(ModGemmArgs a, uint32_t Ppad) {
+__global__ __launch_bounds__(256) void mod_gemm_mfma_kernel(ModGemmArgs a, uint32_t Ppad, int limb0) {
     constexpr int NS = 2 * D - 1;
-    const int l = blockIdx.z;
+    const int l = limb0 + blockIdx.z;
     const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
     const int r = lane & 31, h = lane >> 5;
     const int m0 = blockIdx.y * 64 + (w & 1) * 32;
     const uint32_t p0 = blockIdx.x * 64 + (w >> 1) * 32;
     const int8_t* Al = a.Adig + (uint64_t)l * a.adL;
-    const int8_t* Bl = a.Bdig + (uint64_t)l * D * Ppad * MK;
+    const int8_t* Bl = a.Bdig + (uint64_t)l * a.D * Ppad * MK;   // planes beyond this limb's D are zero
     v16i acc[NS];
 #pragma unroll
     for (int s = 0; s < NS; ++s) acc[s] = v16i{0};
@@ -222,9 +222,42 @@ __global__ __launch_bounds__(256) void mod_gemm_mfma_kernel(ModGemmArgs a, uint3
             for (int j = 0; j < D; ++j) acc[i + j] = __builtin_amdgcn_mfma_i32_32x32x32_i8(av[i], bv[j], acc[i + j], 0, 0, 0);
     }
     // epilogue: C = sum_s acc_s * 256^s mod q
+    uint64_t* Cl = a.C + (uint64_t)l * a.cL;
+    if (a.epi) {
+        // FP64 (every q < 2^50): |acc_s| < 2^26, so z_t = acc_2t + 256 acc_2t+1 (< 2^35) and
+        // y_u = z_2u + 2^16 z_2u+1 (< 2^51) are exact doubles; C = y_0 + sum_u y_u (2^32u mod q), each
+        // product an exact FP64 modmul with a centred constant (|y c / q| < 2^50), then one canonical
+        // reduction -- about 25 FP64 ops per output instead of 2D-1 64-bit Shoup products.
+        const double* ep = a.epi + (uint64_t)l * 8;
+        LimbConst lc;
+        lc.qf = ep[0];
+        lc.qinv = ep[1];
+        const ArithF64 ar(lc);
+        const double c32[3] = {ep[2], ep[3], ep[4]};
+        const uint32_t colf = p0 + r;
+        if (colf >= a.P) return;
+        constexpr int NZ = (NS + 1) / 2, NY = (NZ + 1) / 2;
+#pragma unroll
+        for (int reg = 0; reg < 16; ++reg) {
+            const int row = m0 + (reg & 3) + 8 * (reg >> 2) + 4 * h;
+            double z[NZ];
+#pragma unroll
+            for (int t = 0; t < NZ; ++t)
+                z[t] = 2 * t + 1 < NS ? __fma_rn(256.0, (double)acc[2 * t + 1][reg], (double)acc[2 * t][reg])
+                                      : (double)acc[2 * t][reg];
+            double v = 0.0;
+#pragma unroll
+            for (int u = 0; u < NY; ++u) {
+                const double y = 2 * u + 1 < NZ ? __fma_rn(65536.0, z[2 * u + 1], z[2 * u]) : z[2 * u];
+                v += u == 0 ? y : ar.mulmod(y, c32[u - 1]);
+            }
+            Cl[(uint64_t)row * a.scM + (uint64_t)(colf >> a.log_n) * a.scY + (colf & ((1u << a.log_n) - 1))] = ar.canon(v);
+        }
+        return;
+    }
     const uint64_t q = a.qmu[2 * l], mu = a.qmu[2 * l + 1];
     const uint64_t* rt = a.rtab + (uint64_t)l * NS * 2;
-    uint64_t* C = a.C + (uint64_t)l * a.cL;
+    uint64_t* C = Cl;
     const uint32_t col = p0 + r;
     if (col >= a.P) return;
 #pragma unroll
@@ -264,22 +297,40 @@ void balanced_digits(uint64_t x, int D, int8_t* out) {
 int launch_mod_gemm(const ModGemmArgs& a, int L, hipStream_t s) {
     if (a.Adig && a.M == 512 && a.K == MK) {
         const uint32_t Ppad = (a.P + 63) / 64 * 64;
-        const dim3 gd((Ppad + 255) / 256, MK / 16, L), grid(Ppad / 64, 512 / 64, L);
+        const dim3 gd((Ppad + 255) / 256, MK / 16, L);
         switch (a.D) {
-#define MFHE_MFMA_CASE(d)                                                                                        \
+#define MFHE_DIG_CASE(d)                                                                                         \
     case d:                                                                                                      \
         hipLaunchKernelGGL(mfma_digitize_kernel<d>, gd, dim3(256), 0, s, a.B, a.bL, a.sbK, a.sbY, a.log_n, a.P,   \
                            Ppad, a.Bdig);                                                                        \
-        hipLaunchKernelGGL(mod_gemm_mfma_kernel<d>, grid, dim3(256), 0, s, a, Ppad);                             \
         break;
-            MFHE_MFMA_CASE(5)
-            MFHE_MFMA_CASE(6)
-            MFHE_MFMA_CASE(7)
-            MFHE_MFMA_CASE(8)
-#undef MFHE_MFMA_CASE
+            MFHE_DIG_CASE(5)
+            MFHE_DIG_CASE(6)
+            MFHE_DIG_CASE(7)
+            MFHE_DIG_CASE(8)
+#undef MFHE_DIG_CASE
             default: return set_error(MFHE_EINVAL, "mod_gemm: MFMA digit count must be 5..8");
         }
-        MFHE_CHECK_LAUNCH("mod_gemm_mfma_kernel");
+        MFHE_CHECK_LAUNCH("mfma_digitize_kernel");
+        // one GEMM launch per run of consecutive limbs that need the same number of digits
+        for (int l0 = 0; l0 < L;) {
+            const int d = a.limbD ? std::max(a.limbD[l0], 5) : a.D;
+            int l1 = l0 + 1;
+            while (l1 < L && (a.limbD ? std::max(a.limbD[l1], 5) : a.D) == d) ++l1;
+            const dim3 grid(Ppad / 64, 512 / 64, l1 - l0);
+            switch (d) {
+#define MFHE_MFMA_CASE(dd) \
+    case dd: hipLaunchKernelGGL(mod_gemm_mfma_kernel<dd>, grid, dim3(256), 0, s, a, Ppad, l0); break;
+                MFHE_MFMA_CASE(5)
+                MFHE_MFMA_CASE(6)
+                MFHE_MFMA_CASE(7)
+                MFHE_MFMA_CASE(8)
+#undef MFHE_MFMA_CASE
+                default: return set_error(MFHE_EINVAL, "mod_gemm: MFMA digit count must be 5..8");
+            }
+            MFHE_CHECK_LAUNCH("mod_gemm_mfma_kernel");
+            l0 = l1;
+        }
         return MFHE_OK;
     }
     dim3 grid((a.P + TP - 1) / TP, (a.M + TM - 1) / TM, L);

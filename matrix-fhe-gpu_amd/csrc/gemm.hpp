@@ -31,9 +31,11 @@ struct ModGemmArgs {
     // Adig == nullptr selects the VALU u128 kernel.
     const int8_t* Adig = nullptr;
     uint64_t adL = 0;
-    int D = 0;
+    int D = 0;                   // digit-plane stride (max over limbs)
     const uint64_t* rtab = nullptr;
     int8_t* Bdig = nullptr;
+    const int* limbD = nullptr;  // host: digits limb l needs (<= D); null = D for every limb
+    const double* epi = nullptr; // [L][8] FP64 epilogue (q, 1/q, centred 2^32k mod q); null = integer epilogue
 };
 
 // bytes of B digit workspace the MFMA path needs for P columns and L limbs at D digits

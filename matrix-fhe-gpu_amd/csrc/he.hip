@@ -299,6 +299,9 @@ static int use_mfma(mfhe_ctx* c, ModGemmArgs& a, const uint64_t* A, int L) {
     a.D = c->wD;
     a.rtab = c->d_wrtab;
     a.Bdig = (int8_t*)c->gemm_ws;
+    // a.aL == 0: one A shared by every limb (vector transforms) -> every limb uses the full digit count
+    a.limbD = (a.aL && (int)c->wDl.size() == L) ? c->wDl.data() : nullptr;
+    a.epi = c->d_wepi;
     return MFHE_OK;
 }
 

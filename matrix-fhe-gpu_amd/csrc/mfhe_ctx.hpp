@@ -80,7 +80,9 @@ struct mfhe_ctx {
     int8_t* d_wVdig = nullptr;   // [L][wD][512][512] balanced base-256 digits of V   (i8 MFMA W-CRT)
     int8_t* d_wVidig = nullptr;  // same for V^-1
     uint64_t* d_wrtab = nullptr; // [L][2 wD - 1][2] (256^s mod q, Shoup)
-    int wD = 0;                  // 0: no MFMA tables (some q <= 2^27)
+    int wD = 0;                  // 0: no MFMA tables (some q <= 2^27); else the plane stride (max digits)
+    std::vector<int> wDl;        // digits limb l needs (<= wD): its higher planes are all zero
+    double* d_wepi = nullptr;    // [L][8] FP64 epilogue constants (gemm.hip GemmEpiF), null: integer epilogue
     int wcrt_mfma = 1;           // MFHE_OPT_WCRT_MFMA
     void* gemm_ws = nullptr;     // B digit planes for the MFMA GEMM, grown on demand
     size_t gemm_ws_bytes = 0;
