@@ -41,6 +41,8 @@ def parse():
     ap.add_argument("--ntt-chunk", type=int, default=None, help="MFHE_OPT_NTT_CHUNK_BYTES override (tuning)")
     ap.add_argument("--ntt-fused", type=int, default=None, help="MFHE_OPT_NTT_FUSED override (tuning)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--no-pipeline", action="store_true",
+                    help="skip the reference-geometry encode->encrypt->decrypt->decode line (N=1 only)")
     ap.add_argument("--cpu-seconds", type=float, default=10.0)
     ap.add_argument("--only", default="all", help="all | ntt | crt | recombine (profiling)")
     ap.add_argument("--recombine-batch", type=int, default=256,
@@ -99,6 +101,45 @@ def pmc_traffic(N, L, batch):
     return best
 
 
+def pipeline_line(reps=10):
+    """src/main.cu:31-157 flow at the reference geometry (n = 64, 512 W-lanes, the 11 reference moduli):
+    encode -> encrypt_pair -> decrypt_and_decode, HIP-event timed, with main.cu's 1e-4 check."""
+    import numpy as np
+    import torch
+    import mfhe
+    ctx = mfhe.Context(mfhe.RNS_MODULI, 6, mfhe.CONV_PHANTOM | mfhe.CONV_WCRT)
+    ctx.reserve_workspace()
+    n2 = 64 * 64
+    ell, i = np.meshgrid(np.arange(512), np.arange(n2), indexing="ij")
+    msg = ((ell + i * 1e-5) + 1j * (ell - i * 1e-5)).ravel()          # main.cu:62-69
+    mt = torch.from_numpy(msg.view(np.float64).copy()).cuda()
+    words = 512 * 11 * n2
+    sk = torch.empty(512 * 11 * 64, dtype=torch.int64, device="cuda")
+    re_, im_ = (torch.empty(words, dtype=torch.int64, device="cuda") for _ in range(2))
+    cre, cim = (torch.empty(2 * words, dtype=torch.int64, device="cuda") for _ in range(2))
+    res = torch.empty_like(mt)
+    ctx.keygen(sk)
+
+    def run():
+        ctx.encode(mt, re_, im_)
+        ctx.encrypt_pair(re_, im_, sk, cre, cim)
+        ctx.decrypt_and_decode(cre, cim, sk, res)
+    run()
+    torch.cuda.synchronize()
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    e0.record()
+    for _ in range(reps):
+        run()
+    e1.record()
+    torch.cuda.synchronize()
+    err = float(np.max(np.abs(res.cpu().numpy().view(np.complex128) - msg)))
+    ms = e0.elapsed_time(e1) / reps
+    ctx.close()
+    return {"workload": "encode->encrypt_pair->decrypt_and_decode, n=64 x 512 W-lanes x L=11 (reference geometry)",
+            "ms": round(ms, 3), "messages_per_s": round(512 * n2 / (ms * 1e-3)), "max_err": err,
+            "main_cu_check_1e-4": err < 1e-4}
+
+
 def cpu_baseline(log_n, moduli, seconds):
     """Reference CPU path restated (oracle, Harvey/Shoup phantom NTT, OpenMP over polys)."""
     import numpy as np
@@ -115,13 +156,16 @@ def cpu_baseline(log_n, moduli, seconds):
     t0 = time.perf_counter()
     oracle.phantom_fwd(probe, L, log_n, moduli)
     one = max((time.perf_counter() - t0) / 8, 1e-5)
-    batch = max(1, int(seconds / one))
+    batch = max(8, min(4096, int(1.0 / one)))      # ~1 s per call, repeated until `seconds` have passed
     data = np.tile(data, batch)
-    t0 = time.perf_counter()
-    oracle.phantom_fwd(data, L, log_n, moduli)
-    dt = time.perf_counter() - t0
-    return {"value": batch * L / dt, "unit": "NTT/s", "cores": threads, "kind": "port",
-            "sample": f"{batch}x{L} forward NTTs N=2^{log_n} (oracle phantom Harvey NTT, OpenMP {threads} threads, "
+    done, dt = 0, 0.0
+    while dt < seconds:
+        t0 = time.perf_counter()
+        oracle.phantom_fwd(data, L, log_n, moduli)
+        dt += time.perf_counter() - t0
+        done += batch
+    return {"value": done * L / dt, "unit": "NTT/s", "cores": threads, "kind": "port",
+            "sample": f"{done}x{L} forward NTTs N=2^{log_n} (oracle phantom Harvey NTT, OpenMP {threads} threads, "
                       f"{dt:.1f} s)"}
 
 
@@ -284,6 +328,8 @@ def main():
             out["encode_crt_GBps"] = 16.0 * (L + 1) * N * cb / (res["crt_ev_ms"] * 1e-3) / 1e9
         if "recombine" in res:
             out["residue_shard_ntt_roundtrip_crt_recombine"] = res["recombine"]
+        if world == 1 and not args.no_pipeline and args.only == "all":
+            out["reference_geometry_pipeline"] = pipeline_line()
         if world == 1 and not args.no_cpu_baseline and args.only == "all":
             try:
                 out["cpu_baseline"] = cpu_baseline(log_n, moduli, args.cpu_seconds)
