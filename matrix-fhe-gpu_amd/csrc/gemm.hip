@@ -197,7 +197,7 @@ __global__ __launch_bounds__(256) void mfma_digitize_kernel(const uint64_t* __re
 }
 
 template <int D>
-__global__ __launch_bounds__(256) void mod_gemm_mfma_kernel(ModGemmArgs a, uint32_t Ppad, int limb0) {
+__global__ __launch_bounds__(256, D <= 6 ? 2 : 1) void mod_gemm_mfma_kernel(ModGemmArgs a, uint32_t Ppad, int limb0) {
     constexpr int NS = 2 * D - 1;
     const int l = limb0 + blockIdx.z;
     const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
