@@ -65,8 +65,10 @@ def main():
         quick = os.environ.get("QUICK") == "1"
         for pf in ((0,) if quick else (0, 1)):
             for wg in ((16,) if os.environ.get("WG16") else (0, 16) if quick else (0, 1, 2, 3, 4, 16)):
-                for cb, plan in [(c, p) for c in chunks for p in [int(x) for x in os.environ.get("PLANS", "0").split(",")]]:
+                for cb, plan, ov in [(c, p, o) for c in chunks for p in [int(x) for x in os.environ.get("PLANS", "0").split(",")]
+                                     for o in [int(x) for x in os.environ.get("OVERLAP", "0").split(",")]]:
                     ctx.set_option(2, plan)
+                    ctx.set_option(10, ov)
                     ctx.set_option(OPT_PF, pf)
                     ctx.set_option(OPT_WG, wg)
                     ctx.set_option(mfhe.OPT_NTT_CHUNK_BYTES, cb)
@@ -78,7 +80,7 @@ def main():
                     i = t_call(lambda: ctx.ntt_inv(d, batch=batch))
                     ntts = batch * L
                     print(json.dumps({"logN": log_n, "L": L, "batch": batch, "prefetch": pf, "wg_per_cu": wg,
-                                      "chunk_MiB": cb >> 20, "plan": plan, "fwd_ms": round(f, 4), "fwd_NTT_s": round(ntts / f * 1e3),
+                                      "chunk_MiB": cb >> 20, "plan": plan, "overlap": ov, "fwd_ms": round(f, 4), "fwd_NTT_s": round(ntts / f * 1e3),
                                       "fwd_alg_GBps": round(16 * N * ntts / f / 1e6, 1), "inv_ms": round(i, 4),
                                       "inv_NTT_s": round(ntts / i * 1e3), "roundtrip_ok": ok}), flush=True)
         del d, ref, q
