@@ -68,7 +68,8 @@ def main():
                 for cb, plan, ov in [(c, p, o) for c in chunks for p in [int(x) for x in os.environ.get("PLANS", "0").split(",")]
                                      for o in [int(x) for x in os.environ.get("OVERLAP", "0").split(",")]]:
                     ctx.set_option(2, plan)
-                    ctx.set_option(10, ov)
+                    if os.environ.get("OVERLAP"):
+                        ctx.set_option(10, ov)
                     ctx.set_option(OPT_PF, pf)
                     ctx.set_option(OPT_WG, wg)
                     ctx.set_option(mfhe.OPT_NTT_CHUNK_BYTES, cb)
