@@ -196,32 +196,11 @@ __global__ __launch_bounds__(256) void mfma_digitize_kernel(const uint64_t* __re
     }
 }
 
+// C = sum_s acc_s * 256^s mod q for the 32 x 32 wave tile at (m0, p0) of limb l (lane = (r, h))
 template <int D>
-__global__ __launch_bounds__(256, D <= 6 ? 2 : 1) void mod_gemm_mfma_kernel(ModGemmArgs a, uint32_t Ppad, int limb0) {
+__device__ __forceinline__ void mfma_epilogue(const ModGemmArgs& a, const v16i (&acc)[2 * D - 1], int l, int m0,
+                                              uint32_t p0, int r, int h) {
     constexpr int NS = 2 * D - 1;
-    const int l = limb0 + blockIdx.z;
-    const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
-    const int r = lane & 31, h = lane >> 5;
-    const int m0 = blockIdx.y * 64 + (w & 1) * 32;
-    const uint32_t p0 = blockIdx.x * 64 + (w >> 1) * 32;
-    const int8_t* Al = a.Adig + (uint64_t)l * a.adL;
-    const int8_t* Bl = a.Bdig + (uint64_t)l * a.D * Ppad * MK;   // planes beyond this limb's D are zero
-    v16i acc[NS];
-#pragma unroll
-    for (int s = 0; s < NS; ++s) acc[s] = v16i{0};
-    for (int kc = 0; kc < MK / 32; ++kc) {
-        v4i av[D], bv[D];
-#pragma unroll
-        for (int i = 0; i < D; ++i) {
-            av[i] = *(const v4i*)(Al + ((uint64_t)i * 512 + m0 + r) * MK + kc * 32 + 16 * h);
-            bv[i] = *(const v4i*)(Bl + ((uint64_t)i * Ppad + p0 + r) * MK + kc * 32 + 16 * h);
-        }
-#pragma unroll
-        for (int i = 0; i < D; ++i)
-#pragma unroll
-            for (int j = 0; j < D; ++j) acc[i + j] = __builtin_amdgcn_mfma_i32_32x32x32_i8(av[i], bv[j], acc[i + j], 0, 0, 0);
-    }
-    // epilogue: C = sum_s acc_s * 256^s mod q
     uint64_t* Cl = a.C + (uint64_t)l * a.cL;
     if (a.epi) {
         // FP64 (every q < 2^50): |acc_s| < 2^26, so z_t = acc_2t + 256 acc_2t+1 (< 2^35) and
@@ -277,6 +256,92 @@ __global__ __launch_bounds__(256, D <= 6 ? 2 : 1) void mod_gemm_mfma_kernel(ModG
     }
 }
 
+template <int D>
+__global__ __launch_bounds__(256, D <= 5 ? 2 : 1) void mod_gemm_mfma_kernel(ModGemmArgs a, uint32_t Ppad, int limb0) {
+    constexpr int NS = 2 * D - 1;
+    const int l = limb0 + blockIdx.z;
+    const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+    const int r = lane & 31, h = lane >> 5;
+    const int m0 = blockIdx.y * 64 + (w & 1) * 32;
+    const uint32_t p0 = blockIdx.x * 64 + (w >> 1) * 32;
+    const int8_t* Al = a.Adig + (uint64_t)l * a.adL;
+    const int8_t* Bl = a.Bdig + (uint64_t)l * a.D * Ppad * MK;   // planes beyond this limb's D are zero
+    v16i acc[NS];
+#pragma unroll
+    for (int s = 0; s < NS; ++s) acc[s] = v16i{0};
+    for (int kc = 0; kc < MK / 32; ++kc) {
+        v4i av[D], bv[D];
+#pragma unroll
+        for (int i = 0; i < D; ++i) {
+            av[i] = *(const v4i*)(Al + ((uint64_t)i * 512 + m0 + r) * MK + kc * 32 + 16 * h);
+            bv[i] = *(const v4i*)(Bl + ((uint64_t)i * Ppad + p0 + r) * MK + kc * 32 + 16 * h);
+        }
+#pragma unroll
+        for (int i = 0; i < D; ++i)
+#pragma unroll
+            for (int j = 0; j < D; ++j) acc[i + j] = __builtin_amdgcn_mfma_i32_32x32x32_i8(av[i], bv[j], acc[i + j], 0, 0, 0);
+    }
+    mfma_epilogue<D>(a, acc, l, m0, p0, r, h);
+}
+
+// LDS-staged variant (default).  Same digit planes, tile (64 x 64 outputs, four 32 x 32 wave tiles) and
+// exact accumulation as mod_gemm_mfma_kernel, but each 32-wide K step of both operands is copied once
+// per workgroup into a double-buffered LDS stage (waves 0-1: A planes, waves 2-3: B planes, 16 B per lane)
+// one step ahead of the MFMAs that consume it: every fragment leaves global memory once per workgroup
+// instead of once per wave, and the next step's global latency overlaps this step's MFMAs.
+template <int D>
+__global__ __launch_bounds__(256, D <= 5 ? 2 : 1) void mod_gemm_mfma_lds_kernel(ModGemmArgs a, uint32_t Ppad, int limb0) {
+    constexpr int NS = 2 * D - 1;
+    constexpr int KS = 32;
+    constexpr int PLANE = 64 * KS;               // one digit plane of one operand per stage (bytes)
+    constexpr int STAGE = 2 * D * PLANE;         // A planes then B planes
+    __shared__ __attribute__((aligned(16))) int8_t lds[2 * STAGE];
+    const int l = limb0 + blockIdx.z;
+    const int t = threadIdx.x, lane = t & 63, w = t >> 6;
+    const int r = lane & 31, h = lane >> 5;
+    const int mb = blockIdx.y * 64, pb = blockIdx.x * 64;
+    const int wm = (w & 1) * 32, wp = (w >> 1) * 32;
+    // loader: t < 128 copies A rows, t >= 128 B columns; (row|col) = (t & 127) >> 1, 16-k half = t & 1
+    const bool ldA = t < 128;
+    const int lr = (t & 127) >> 1, lh = t & 1;
+    const int8_t* src = ldA ? a.Adig + (uint64_t)l * a.adL + (uint64_t)(mb + lr) * MK
+                            : a.Bdig + (uint64_t)l * a.D * Ppad * MK + (uint64_t)(pb + lr) * MK;
+    const uint64_t pstride = ldA ? (uint64_t)512 * MK : (uint64_t)Ppad * MK;   // digit-plane stride
+    const int dst0 = (ldA ? 0 : D * PLANE) + lr * KS + 16 * lh;
+    v4i pre[D];
+    auto fetch = [&](int kc) {
+#pragma unroll
+        for (int i = 0; i < D; ++i) pre[i] = *(const v4i*)(src + i * pstride + kc * KS + 16 * lh);
+    };
+    auto stash = [&](int buf) {
+#pragma unroll
+        for (int i = 0; i < D; ++i) *(v4i*)(lds + buf * STAGE + dst0 + i * PLANE) = pre[i];
+    };
+    v16i acc[NS];
+#pragma unroll
+    for (int s = 0; s < NS; ++s) acc[s] = v16i{0};
+    fetch(0);
+    stash(0);
+    __syncthreads();
+    for (int kc = 0; kc < MK / KS; ++kc) {
+        const int buf = kc & 1;
+        if (kc + 1 < MK / KS) fetch(kc + 1);
+        const int8_t* st = lds + buf * STAGE;
+        v4i bv[D];
+#pragma unroll
+        for (int j = 0; j < D; ++j) bv[j] = *(const v4i*)(st + (D + j) * PLANE + (wp + r) * KS + 16 * h);
+#pragma unroll
+        for (int i = 0; i < D; ++i) {
+            const v4i av = *(const v4i*)(st + i * PLANE + (wm + r) * KS + 16 * h);
+#pragma unroll
+            for (int j = 0; j < D; ++j) acc[i + j] = __builtin_amdgcn_mfma_i32_32x32x32_i8(av, bv[j], acc[i + j], 0, 0, 0);
+        }
+        if (kc + 1 < MK / KS) stash(buf ^ 1);   // readers of buf ^ 1 all passed the previous barrier
+        __syncthreads();
+    }
+    mfma_epilogue<D>(a, acc, l, mb + wm, (uint32_t)(pb + wp), r, h);
+}
+
 size_t mod_gemm_mfma_ws(uint32_t P, int L, int D) {
     const uint64_t Ppad = ((uint64_t)P + 63) / 64 * 64;
     return (size_t)L * D * Ppad * MK;
@@ -319,8 +384,11 @@ int launch_mod_gemm(const ModGemmArgs& a, int L, hipStream_t s) {
             while (l1 < L && (a.limbD ? std::max(a.limbD[l1], 5) : a.D) == d) ++l1;
             const dim3 grid(Ppad / 64, 512 / 64, l1 - l0);
             switch (d) {
-#define MFHE_MFMA_CASE(dd) \
-    case dd: hipLaunchKernelGGL(mod_gemm_mfma_kernel<dd>, grid, dim3(256), 0, s, a, Ppad, l0); break;
+#define MFHE_MFMA_CASE(dd)                                                                                    \
+    case dd:                                                                                                  \
+        if (a.lds_stage) hipLaunchKernelGGL(mod_gemm_mfma_lds_kernel<dd>, grid, dim3(256), 0, s, a, Ppad, l0); \
+        else hipLaunchKernelGGL(mod_gemm_mfma_kernel<dd>, grid, dim3(256), 0, s, a, Ppad, l0);                 \
+        break;
                 MFHE_MFMA_CASE(5)
                 MFHE_MFMA_CASE(6)
                 MFHE_MFMA_CASE(7)

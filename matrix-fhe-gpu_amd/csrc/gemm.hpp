@@ -36,6 +36,7 @@ struct ModGemmArgs {
     int8_t* Bdig = nullptr;
     const int* limbD = nullptr;  // host: digits limb l needs (<= D); null = D for every limb
     const double* epi = nullptr; // [L][8] FP64 epilogue (q, 1/q, centred 2^32k mod q); null = integer epilogue
+    bool lds_stage = true;       // LDS-staged MFMA kernel (false: fragments straight from global memory)
 };
 
 // bytes of B digit workspace the MFMA path needs for P columns and L limbs at D digits

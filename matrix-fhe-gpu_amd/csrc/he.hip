@@ -302,6 +302,7 @@ static int use_mfma(mfhe_ctx* c, ModGemmArgs& a, const uint64_t* A, int L) {
     // a.aL == 0: one A shared by every limb (vector transforms) -> every limb uses the full digit count
     a.limbD = (a.aL && (int)c->wDl.size() == L) ? c->wDl.data() : nullptr;
     a.epi = c->d_wepi;
+    a.lds_stage = c->wcrt_mfma != 2;
     return MFHE_OK;
 }
 

@@ -395,7 +395,7 @@ def test_wcrt_mfma_matches_valu_and_oracle(mfhe, orc, n, L):
     rng = np.random.default_rng(n * 100 + L)
     x = _rand_mat(rng, n, L)
     outs = {}
-    for mf in (1, 0):
+    for mf in (1, 2, 0):
         ctx.set_option(mfhe.OPT_WCRT_MFMA, mf)
         d = _dev(mfhe, x)
         f = torch.empty_like(d)
@@ -410,8 +410,9 @@ def test_wcrt_mfma_matches_valu_and_oracle(mfhe, orc, n, L):
         np.testing.assert_array_equal(outs[mf][1], x)
         rng = np.random.default_rng(n * 100 + L)   # same vector input for both runs
         _rand_mat(rng, n, L)
-    for a, b in zip(outs[1], outs[0]):
-        np.testing.assert_array_equal(a, b)
+    for mf in (1, 2):
+        for a, b in zip(outs[mf], outs[0]):
+            np.testing.assert_array_equal(a, b)
     if n <= 8:
         h = orc.HE(n, RNS[:L], 2.0 ** 35)
         ref = np.zeros_like(x)
