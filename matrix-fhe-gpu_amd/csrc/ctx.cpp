@@ -261,10 +261,12 @@ static int build_wcrt(mfhe_ctx* c) {
         for (int l = 0; l < L; ++l) {
             int8_t d[8];
             for (size_t e = 0; e < plane; ++e) {
+                // plane layout [k/32][row][k%32] (gemm.hip "k-panel-major"): row = w, k = r of V[w][r]
+                const size_t w = e / PHI, r = e % PHI, o = ((r >> 5) * PHI + w) * 32 + (r & 31);
                 balanced_digits(V[(size_t)l * plane + e], D, d);
-                for (int i = 0; i < D; ++i) vd[((size_t)l * D + i) * plane + e] = d[i];
+                for (int i = 0; i < D; ++i) vd[((size_t)l * D + i) * plane + o] = d[i];
                 balanced_digits(Vi[(size_t)l * plane + e], D, d);
-                for (int i = 0; i < D; ++i) vid[((size_t)l * D + i) * plane + e] = d[i];
+                for (int i = 0; i < D; ++i) vid[((size_t)l * D + i) * plane + o] = d[i];
             }
             const uint64_t q = c->moduli[l];
             uint64_t p256 = 1;

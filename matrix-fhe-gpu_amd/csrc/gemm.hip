@@ -162,37 +162,41 @@ constexpr int MK = 512;   // K of the W-CRT GEMM
 using v4i = int __attribute__((ext_vector_type(4)));
 using v16i = int __attribute__((ext_vector_type(16)));
 
-// one thread: column p (of Ppad; zero past P), 16 consecutive k; B (k, p) via the (sbK, sbY, log_n) map
+// Digit planes are "k-panel-major": [K/32][rows][32] bytes, so one 32-k panel of 64 consecutive rows (or
+// columns) is 2 KiB of contiguous memory: every fragment load (16 B per lane, lanes over rows and k halves)
+// and every digitize store below is a fully coalesced sweep.
+//
+// one thread: column p (of Ppad; zero past P), one 32-k panel; B (k, p) via the (sbK, sbY, log_n) map
 template <int D>
 __global__ __launch_bounds__(256) void mfma_digitize_kernel(const uint64_t* __restrict__ B, uint64_t bL,
                                                             uint64_t sbK, uint64_t sbY, int log_n, uint32_t P,
                                                             uint32_t Ppad, int8_t* __restrict__ out) {
     const uint32_t p = blockIdx.x * 256 + threadIdx.x;
-    const int k0 = blockIdx.y * 16;
+    const int kc = blockIdx.y;
     const int l = blockIdx.z;
     if (p >= Ppad) return;
-    int8_t dig[D][16];
     const uint64_t* Bl = B + (uint64_t)l * bL;
     const uint64_t col = (uint64_t)(p >> log_n) * sbY + (p & ((1u << log_n) - 1));
+    uint32_t pk[D][8];   // plane i, bytes 4c..4c+3 of the panel's 32 k (byte v is the digit mod 256)
 #pragma unroll
-    for (int kk = 0; kk < 16; ++kk) {
-        uint64_t x = p < P ? Bl[(uint64_t)(k0 + kk) * sbK + col] : 0;
+    for (int i = 0; i < D; ++i)
+#pragma unroll
+        for (int c = 0; c < 8; ++c) pk[i][c] = 0;
+#pragma unroll
+    for (int kk = 0; kk < 32; ++kk) {
+        uint64_t x = p < P ? Bl[(uint64_t)(kc * 32 + kk) * sbK + col] : 0;
 #pragma unroll
         for (int i = 0; i < D; ++i) {
-            int v = (int)(x & 255);
-            x >>= 8;
-            if (v >= 128) {
-                v -= 256;
-                ++x;
-            }
-            dig[i][kk] = (int8_t)v;
+            const uint32_t v = (uint32_t)x & 255u;
+            x = (x >> 8) + (v >> 7);                 // balanced digits: v >= 128 stands for v - 256
+            pk[i][kk >> 2] |= v << (8 * (kk & 3));
         }
     }
 #pragma unroll
     for (int i = 0; i < D; ++i) {
-        v4i v;
-        __builtin_memcpy(&v, dig[i], 16);
-        *(v4i*)(out + ((((uint64_t)l * D + i) * Ppad + p) * MK + k0)) = v;
+        int8_t* o = out + (((uint64_t)l * D + i) * (MK / 32) + kc) * Ppad * 32 + (uint64_t)p * 32;
+        *(v4i*)o = v4i{(int)pk[i][0], (int)pk[i][1], (int)pk[i][2], (int)pk[i][3]};
+        *(v4i*)(o + 16) = v4i{(int)pk[i][4], (int)pk[i][5], (int)pk[i][6], (int)pk[i][7]};
     }
 }
 
@@ -273,8 +277,8 @@ __global__ __launch_bounds__(256, D <= 5 ? 2 : 1) void mod_gemm_mfma_kernel(ModG
         v4i av[D], bv[D];
 #pragma unroll
         for (int i = 0; i < D; ++i) {
-            av[i] = *(const v4i*)(Al + ((uint64_t)i * 512 + m0 + r) * MK + kc * 32 + 16 * h);
-            bv[i] = *(const v4i*)(Bl + ((uint64_t)i * Ppad + p0 + r) * MK + kc * 32 + 16 * h);
+            av[i] = *(const v4i*)(Al + (uint64_t)i * 512 * MK + ((uint64_t)kc * 512 + m0 + r) * 32 + 16 * h);
+            bv[i] = *(const v4i*)(Bl + (uint64_t)i * Ppad * MK + ((uint64_t)kc * Ppad + p0 + r) * 32 + 16 * h);
         }
 #pragma unroll
         for (int i = 0; i < D; ++i)
@@ -304,14 +308,15 @@ __global__ __launch_bounds__(256, D <= 5 ? 2 : 1) void mod_gemm_mfma_lds_kernel(
     // loader: t < 128 copies A rows, t >= 128 B columns; (row|col) = (t & 127) >> 1, 16-k half = t & 1
     const bool ldA = t < 128;
     const int lr = (t & 127) >> 1, lh = t & 1;
-    const int8_t* src = ldA ? a.Adig + (uint64_t)l * a.adL + (uint64_t)(mb + lr) * MK
-                            : a.Bdig + (uint64_t)l * a.D * Ppad * MK + (uint64_t)(pb + lr) * MK;
-    const uint64_t pstride = ldA ? (uint64_t)512 * MK : (uint64_t)Ppad * MK;   // digit-plane stride
+    const uint64_t rows = ldA ? 512 : Ppad;                        // rows of the operand's planes
+    const int8_t* src = (ldA ? a.Adig + (uint64_t)l * a.adL : a.Bdig + (uint64_t)l * a.D * Ppad * MK) +
+                        (uint64_t)((ldA ? mb : pb) + lr) * 32 + 16 * lh;
+    const uint64_t pstride = rows * MK;                             // digit-plane stride
     const int dst0 = (ldA ? 0 : D * PLANE) + lr * KS + 16 * lh;
     v4i pre[D];
     auto fetch = [&](int kc) {
 #pragma unroll
-        for (int i = 0; i < D; ++i) pre[i] = *(const v4i*)(src + i * pstride + kc * KS + 16 * lh);
+        for (int i = 0; i < D; ++i) pre[i] = *(const v4i*)(src + i * pstride + (uint64_t)kc * rows * 32);
     };
     auto stash = [&](int buf) {
 #pragma unroll
@@ -362,7 +367,7 @@ void balanced_digits(uint64_t x, int D, int8_t* out) {
 int launch_mod_gemm(const ModGemmArgs& a, int L, hipStream_t s) {
     if (a.Adig && a.M == 512 && a.K == MK) {
         const uint32_t Ppad = (a.P + 63) / 64 * 64;
-        const dim3 gd((Ppad + 255) / 256, MK / 16, L);
+        const dim3 gd((Ppad + 255) / 256, MK / 32, L);
         switch (a.D) {
 #define MFHE_DIG_CASE(d)                                                                                         \
     case d:                                                                                                      \
