@@ -30,7 +30,7 @@ def main():
     calls = [fwd[i * per:(i + 1) * per] for i in range(W + S)][W:]
     kern_ms = [sum(int(r["End_Timestamp"]) - int(r["Start_Timestamp"]) for r in c) / 1e6 for c in calls]
     span_ms = [(int(c[-1]["End_Timestamp"]) - int(c[0]["Start_Timestamp"])) / 1e6 for c in calls]
-    names = sorted({r["Kernel_Name"] for r in fwd})
+    names = sorted({r["Kernel_Name"] for c in calls for r in c})
     per_kernel = {}
     for n in names:
         durs = [int(r["End_Timestamp"]) - int(r["Start_Timestamp"]) for c in calls for r in c if r["Kernel_Name"] == n]
