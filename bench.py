@@ -42,7 +42,7 @@ def parse():
     ap.add_argument("--ntt-fused", type=int, default=None, help="MFHE_OPT_NTT_FUSED override (tuning)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-pipeline", action="store_true",
-                    help="skip the reference-geometry encode->encrypt->decrypt->decode line (N=1 only)")
+                    help="skip the reference-geometry pipeline and other-config NTT lines (N=1 only)")
     ap.add_argument("--cpu-seconds", type=float, default=10.0)
     ap.add_argument("--only", default="all", help="all | ntt | crt | recombine (profiling)")
     ap.add_argument("--recombine-batch", type=int, default=256,
@@ -99,6 +99,44 @@ def pmc_traffic(N, L, batch):
         if (c.get("N"), c.get("limbs"), c.get("batch")) == (N, L, batch) and "fwd_traffic_bytes_per_transform" in d:
             best = (d["fwd_traffic_bytes_per_transform"], Path(f).name)
     return best
+
+
+def other_configs_line(reps=10):
+    """The other BASELINE.json NTT shapes on this one GPU (parity cases, not the headline): C2 whole, and the
+    per-GPU residue shard of C4 (4 GPUs) and C5 (8 GPUs).  Forward and inverse NTT/s, HIP events."""
+    import torch
+    import mfhe
+    res = {}
+    for name, log_n, L, lg, batch in (("C2: N=2^14 L=4 batch 256", 14, 4, 4, 256),
+                                     ("C4 shard: N=2^16 L=16 (4 of 16 limbs) batch 1024", 16, 16, 4, 1024),
+                                     ("C5 shard: N=2^17 L=32 (4 of 32 limbs) batch 4096", 17, 32, 4, 4096)):
+        N = 1 << log_n
+        moduli = gen_moduli(50, 1 << (log_n + 2), L)
+        ctx = mfhe.Context(moduli, log_n, mfhe.CONV_PHANTOM)
+        d = torch.empty(batch * lg * N, dtype=torch.int64, device="cuda")
+        qt = torch.tensor(moduli[:lg], dtype=torch.int64, device="cuda").repeat_interleave(N).repeat(batch)
+        d.random_(0, 2 ** 62).remainder_(qt)
+        del qt
+        out = {}
+        for kind, fn in (("fwd", ctx.ntt_fwd), ("inv", ctx.ntt_inv)):
+            fn(d, batch=batch, start_limb=0, nlimbs=lg)
+            torch.cuda.synchronize()
+            e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            e0.record()
+            for _ in range(reps):
+                fn(d, batch=batch, start_limb=0, nlimbs=lg)
+            e1.record()
+            torch.cuda.synchronize()
+            ms = e0.elapsed_time(e1) / reps
+            rate = batch * lg / (ms * 1e-3)
+            out[f"{kind}_NTT_per_s"] = round(rate)
+            out[f"{kind}_alg_GBps"] = round(16.0 * N * rate / 1e9, 1)
+        out["frac_fwd"] = round(out["fwd_alg_GBps"] / HBM_PEAK_GBS, 4)
+        out["working_set_GiB"] = round(batch * lg * N * 8 / 2 ** 30, 3)
+        res[name] = out
+        del d
+        ctx.close()
+    return res
 
 
 def pipeline_line(reps=10):
@@ -342,6 +380,7 @@ def main():
             out["residue_shard_ntt_roundtrip_crt_recombine"] = res["recombine"]
         if world == 1 and not args.no_pipeline and args.only == "all":
             out["reference_geometry_pipeline"] = pipeline_line()
+            out["other_ntt_configs"] = other_configs_line()
         if world == 1 and not args.no_cpu_baseline and args.only == "all":
             try:
                 out["cpu_baseline"] = cpu_baseline(log_n, moduli, args.cpu_seconds)
