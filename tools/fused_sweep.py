@@ -26,9 +26,11 @@ def main():
         q = torch.tensor(ctx.moduli, dtype=torch.int64, device="cuda").repeat_interleave(N).repeat(batch)
         d = torch.randint(0, 2 ** 62, (batch * L * N,), dtype=torch.int64, device="cuda") % q
         ref = d.clone()
-        ctx.set_option(OPT_FUSED, 1)
+        import os
+        mode = int(os.environ.get("FUSED_MODE", "1"))
+        ctx.set_option(OPT_FUSED, mode)
         for wg in (1, 2, 3, 4):
-            for lag in (1, 2, 3, 4, 6, 8):
+            for lag in ((1, 2, 3, 4, 6, 8) if mode == 1 else (1,)):
                 ctx.set_option(OPT_WG, wg)
                 ctx.set_option(OPT_LAG, lag)
                 ctx.ntt_fwd(d, batch=batch)
@@ -38,7 +40,7 @@ def main():
                 f = t_call(lambda: ctx.ntt_fwd(d, batch=batch))
                 i = t_call(lambda: ctx.ntt_inv(d, batch=batch))
                 ntts = batch * L
-                print(json.dumps({"logN": log_n, "L": L, "batch": batch, "wg": wg, "lag": lag, "fwd_ms": round(f, 4),
+                print(json.dumps({"logN": log_n, "L": L, "batch": batch, "mode": mode, "wg": wg, "lag": lag, "fwd_ms": round(f, 4),
                                   "fwd_NTT_s": round(ntts / f * 1e3), "inv_NTT_s": round(ntts / i * 1e3),
                                   "ok": ok}), flush=True)
 
