@@ -124,21 +124,52 @@ __global__ __launch_bounds__(256) void mul_s_kernel(const uint64_t* __restrict__
     t[idx] = r >= q ? r - q : r;
 }
 
-// combine_b_kernel HE.cu:535-547 (b = m - t + e) and add_poly_kernel HE.cu:549-560 (b + t)
-__global__ void combine_kernel(const uint64_t* m, const uint64_t* t, const uint64_t* e, uint64_t* b,
-                               const uint64_t* qmu, int L, int log_n, uint64_t total, int add) {
-    const uint64_t idx = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x;
-    if (idx >= total) return;
-    const int l = (int)((idx % ((uint64_t)L << log_n)) >> log_n);
+// encrypt epilogue, fused: for matrix-major index i (x, y, l, w) and its poly-major index p,
+//   ct_k.b[i] = m_k[i] - t[p] + e[p] mod q   (combine_b_kernel HE.cu:535-547, then poly_to_matrix)
+//   ct_k.a[i] = a_eval[p]                   (the shared a, poly_to_matrix)
+// for k = re (and im when given) in one pass: 3 + 2 reads and 2 + 2 writes instead of the 20 array
+// passes of layout -> combine -> layout -> layout per component.
+__global__ __launch_bounds__(256) void enc_combine_kernel(const uint64_t* __restrict__ m_re,
+                                                          const uint64_t* __restrict__ m_im,
+                                                          const uint64_t* __restrict__ t, const uint64_t* __restrict__ e,
+                                                          const uint64_t* __restrict__ aev, uint64_t* __restrict__ ct_re,
+                                                          uint64_t* __restrict__ ct_im, const uint64_t* __restrict__ qmu,
+                                                          int log_n, int L, uint64_t total) {
+    const uint64_t i = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x;   // matrix-major index
+    if (i >= total) return;
+    const uint64_t n = 1ull << log_n;
+    const uint64_t x = i & (n - 1), y = (i >> log_n) & (n - 1);
+    const uint64_t wl = i >> (2 * log_n), l = wl % L, w = wl / L;
+    const uint64_t p = ((w * n + y) * L + l) * n + x;
     const uint64_t q = qmu[2 * l];
-    if (add) {
-        const uint64_t s = m[idx] + t[idx];
-        b[idx] = s >= q ? s - q : s;
-    } else {
-        uint64_t d = m[idx] >= t[idx] ? m[idx] - t[idx] : m[idx] + q - t[idx];
-        d += e[idx];
-        b[idx] = d >= q ? d - q : d;
+    const uint64_t tv = t[p], ev = e[p], av = aev[p];
+    auto bval = [&](uint64_t m) {
+        uint64_t d = m >= tv ? m - tv : m + q - tv;
+        d += ev;
+        return d >= q ? d - q : d;
+    };
+    ct_re[i] = bval(m_re[i]);
+    ct_re[total + i] = av;
+    if (m_im) {
+        ct_im[i] = bval(m_im[i]);
+        ct_im[total + i] = av;
     }
+}
+
+// decrypt epilogue, fused: out[p] = ct.b[i] + t[p] mod q (matrix_to_poly of b, then add_poly_kernel
+// HE.cu:549-560), over the poly-major index p.
+__global__ __launch_bounds__(256) void dec_combine_kernel(const uint64_t* __restrict__ ctb, const uint64_t* __restrict__ t,
+                                                          uint64_t* __restrict__ out, const uint64_t* __restrict__ qmu,
+                                                          int log_n, int L, uint64_t total) {
+    const uint64_t p = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x;   // poly-major index [w n + y][l][x]
+    if (p >= total) return;
+    const uint64_t n = 1ull << log_n;
+    const uint64_t x = p & (n - 1), rest = p >> log_n, l = rest % L, wy = rest / L;
+    const uint64_t y = wy & (n - 1), w = wy >> log_n;
+    const uint64_t i = (((w * L + l) << log_n) + y) * n + x;            // matrix-major [w][l][y][x]
+    const uint64_t q = qmu[2 * l];
+    const uint64_t sum = ctb[i] + t[p];
+    out[p] = sum >= q ? sum - q : sum;
 }
 
 // centred int64 -> RNS matrix-major (centered_int_to_rns_matrix_kernel HE.cu:815-835)
@@ -443,7 +474,6 @@ static int encrypt_impl(mfhe_ctx* c, const uint64_t* m_re, const uint64_t* m_im,
     RC(ensure_ws(c));
     const Geo2 g = geo(c);
     Bump b{(char*)c->ws};
-    uint64_t* mp = b.get<uint64_t>(g.words);
     uint64_t* ap = b.get<uint64_t>(g.words);
     uint64_t* aev = b.get<uint64_t>(g.words);
     uint64_t* ant = b.get<uint64_t>(g.words);
@@ -467,27 +497,17 @@ static int encrypt_impl(mfhe_ctx* c, const uint64_t* m_re, const uint64_t* m_im,
                        c->f64_ok ? c->d_limbs : nullptr, g.L, g.logn, (uint32_t)W);
     MFHE_CHECK_LAUNCH("mul_s_kernel");
     RC(mfhe_ntt_inv(c, t, 512 * g.n, 0, g.L, (mfhe_stream_t)s));
-    const uint64_t* ms[2] = {m_re, m_im};
-    uint64_t* cts[2] = {ct_re, ct_im};
-    for (int k = 0; k < 2; ++k) {
-        if (!ms[k]) continue;
-        RC(layout(c, ms[k], mp, true, s));
-        hipLaunchKernelGGL(combine_kernel, g1(W), dim3(256), 0, s, mp, t, eev, ant /*b poly*/, c->d_rns_mu, g.L,
-                           g.logn, W, 0);
-        MFHE_CHECK_LAUNCH("combine_kernel");
-        RC(layout(c, ant, cts[k], false, s));          // b
-        RC(layout(c, aev, cts[k] + W, false, s));      // a (shared)
-    }
+    hipLaunchKernelGGL(enc_combine_kernel, g1(W), dim3(256), 0, s, m_re, m_im, t, eev, aev, ct_re, ct_im,
+                       c->d_rns_mu, g.logn, g.L, W);
+    MFHE_CHECK_LAUNCH("enc_combine_kernel");
     return MFHE_OK;
 }
 
 static int decrypt_impl(mfhe_ctx* c, const uint64_t* ct, const uint64_t* sk, uint64_t* out, hipStream_t s, Bump* pb) {
     const Geo2 g = geo(c);
     const uint64_t W = g.words;
-    uint64_t* bp = pb->get<uint64_t>(W);
     uint64_t* ap = pb->get<uint64_t>(W);
     uint64_t* t = pb->get<uint64_t>(W);
-    RC(layout(c, ct, bp, true, s));
     RC(layout(c, ct + W, ap, true, s));
     RC(mfhe_ntt_fwd(c, ap, 512 * g.n, 0, g.L, (mfhe_stream_t)s));
     if (W >= (1ull << 32)) return set_error(MFHE_EUNSUPPORTED, "ciphertext of 2^32 words or more");
@@ -495,8 +515,8 @@ static int decrypt_impl(mfhe_ctx* c, const uint64_t* ct, const uint64_t* sk, uin
                        c->f64_ok ? c->d_limbs : nullptr, g.L, g.logn, (uint32_t)W);
     MFHE_CHECK_LAUNCH("mul_s_kernel");
     RC(mfhe_ntt_inv(c, t, 512 * g.n, 0, g.L, (mfhe_stream_t)s));
-    hipLaunchKernelGGL(combine_kernel, g1(W), dim3(256), 0, s, bp, t, nullptr, out, c->d_rns_mu, g.L, g.logn, W, 1);
-    MFHE_CHECK_LAUNCH("combine_kernel");
+    hipLaunchKernelGGL(dec_combine_kernel, g1(W), dim3(256), 0, s, ct, t, out, c->d_rns_mu, g.logn, g.L, W);
+    MFHE_CHECK_LAUNCH("dec_combine_kernel");
     return MFHE_OK;
 }
 
