@@ -22,6 +22,9 @@ def main():
     t0 = time.perf_counter()
     ctx = mfhe.Context(mfhe.RNS_MODULI, 6, mfhe.CONV_PHANTOM | mfhe.CONV_WCRT)
     ctx.reserve_workspace()
+    import os
+    if os.environ.get("MFHE_WCRT_MODE"):
+        ctx.set_option(9, int(os.environ["MFHE_WCRT_MODE"]))   # MFHE_OPT_WCRT_MFMA
     t_ctx = time.perf_counter() - t0
     n2 = 64 * 64
     ell, i = np.meshgrid(np.arange(512), np.arange(n2), indexing="ij")
