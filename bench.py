@@ -14,7 +14,6 @@ Run: python bench.py [--gpus N --steps K --warmup W]
 from __future__ import annotations
 
 import argparse
-import ctypes
 import json
 import os
 import sys

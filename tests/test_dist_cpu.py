@@ -60,18 +60,20 @@ def _rank(rank, world, port, mode, q):
         dist.destroy_process_group()
 
 
+@pytest.mark.parametrize("world", [2, 4])
 @pytest.mark.parametrize("mode", ["allgather", "alltoall"])
-def test_residue_shard_exchange_world2(mode):
+def test_residue_shard_exchange(mode, world):
+    """world 2 and 4 (the C4 config shards 16 limbs over 4 GPUs; here 4 limbs, one per rank)."""
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _free_port()
-    procs = [ctx.Process(target=_rank, args=(r, 2, port, mode, q)) for r in range(2)]
+    procs = [ctx.Process(target=_rank, args=(r, world, port, mode, q)) for r in range(world)]
     for p in procs:
         p.start()
     res = dict(q.get(timeout=120) for _ in procs)
     for p in procs:
         p.join(timeout=60)
-    assert res == {0: True, 1: True}
+    assert res == {r: True for r in range(world)}
 
 
 def test_limb_range_rejects_uneven():
