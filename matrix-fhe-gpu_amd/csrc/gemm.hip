@@ -289,15 +289,19 @@ __global__ __launch_bounds__(256, D <= 5 ? 2 : 1) void mod_gemm_mfma_kernel(ModG
 }
 
 // LDS-staged variant (default).  Same digit planes, tile (64 x 64 outputs, four 32 x 32 wave tiles) and
-// exact accumulation as mod_gemm_mfma_kernel, but each 32-wide K step of both operands is copied once
-// per workgroup into a double-buffered LDS stage (waves 0-1: A planes, waves 2-3: B planes, 16 B per lane)
-// one step ahead of the MFMAs that consume it: every fragment leaves global memory once per workgroup
-// instead of once per wave, and the next step's global latency overlaps this step's MFMAs.
+// exact accumulation as mod_gemm_mfma_kernel, but each 64-deep K stage (two 32-k panels) of both operands
+// goes global -> LDS once per workgroup by LDS-DMA (global_load_lds_dwordx4: no VGPR staging; the
+// k-panel-major planes make each wave's 1 KiB destination lane-linear, as the DMA requires), double-
+// buffered one stage ahead of the MFMAs that read it.  Waves 0-1 move A's planes, waves 2-3 B's.
+// RAW order for the DMA'd bytes: issuing waves' s_waitcnt vmcnt(0), then the barrier, then the reads.
+typedef __attribute__((address_space(3))) void* lds_ptr_t;
+
 template <int D>
 __global__ __launch_bounds__(256, D <= 5 ? 2 : 1) void mod_gemm_mfma_lds_kernel(ModGemmArgs a, uint32_t Ppad, int limb0) {
     constexpr int NS = 2 * D - 1;
-    constexpr int KS = 32;
-    constexpr int PLANE = 64 * KS;               // one digit plane of one operand per stage (bytes)
+    constexpr int KS = 64;                       // K per stage: two 32-k panels
+    constexpr int PANEL = 64 * 32;               // 64 rows x 32 k of one digit plane (bytes)
+    constexpr int PLANE = 2 * PANEL;             // one digit plane of one operand per stage
     constexpr int STAGE = 2 * D * PLANE;         // A planes then B planes
     __shared__ __attribute__((aligned(16))) int8_t lds[2 * STAGE];
     const int l = limb0 + blockIdx.z;
@@ -305,43 +309,48 @@ __global__ __launch_bounds__(256, D <= 5 ? 2 : 1) void mod_gemm_mfma_lds_kernel(
     const int r = lane & 31, h = lane >> 5;
     const int mb = blockIdx.y * 64, pb = blockIdx.x * 64;
     const int wm = (w & 1) * 32, wp = (w >> 1) * 32;
-    // loader: t < 128 copies A rows, t >= 128 B columns; (row|col) = (t & 127) >> 1, 16-k half = t & 1
+    // DMA slot li: bytes [16 li, 16 li + 16) of a 2 KiB panel image (row li / 2, k half li & 1)
     const bool ldA = t < 128;
-    const int lr = (t & 127) >> 1, lh = t & 1;
+    const int li = t & 127;
     const uint64_t rows = ldA ? 512 : Ppad;                        // rows of the operand's planes
     const int8_t* src = (ldA ? a.Adig + (uint64_t)l * a.adL : a.Bdig + (uint64_t)l * a.D * Ppad * MK) +
-                        (uint64_t)((ldA ? mb : pb) + lr) * 32 + 16 * lh;
-    const uint64_t pstride = rows * MK;                             // digit-plane stride
-    const int dst0 = (ldA ? 0 : D * PLANE) + lr * KS + 16 * lh;
-    v4i pre[D];
-    auto fetch = [&](int kc) {
+                        (uint64_t)(ldA ? mb : pb) * 32 + li * 16;
+    const uint64_t pstride = rows * MK, kstride = rows * 32;      // digit-plane / k-panel strides
+    const int wbase = (ldA ? 0 : D * PLANE) + (li & ~63) * 16;     // this wave's LDS destination base
+    auto issue = [&](int s, int buf) {
 #pragma unroll
-        for (int i = 0; i < D; ++i) pre[i] = *(const v4i*)(src + i * pstride + (uint64_t)kc * rows * 32);
-    };
-    auto stash = [&](int buf) {
+        for (int i = 0; i < D; ++i)
 #pragma unroll
-        for (int i = 0; i < D; ++i) *(v4i*)(lds + buf * STAGE + dst0 + i * PLANE) = pre[i];
+            for (int pp = 0; pp < 2; ++pp)
+                __builtin_amdgcn_global_load_lds((const void*)(src + i * pstride + (uint64_t)(2 * s + pp) * kstride),
+                                                 (lds_ptr_t)(lds + buf * STAGE + wbase + i * PLANE + pp * PANEL), 16,
+                                                 0, 0);
     };
     v16i acc[NS];
 #pragma unroll
     for (int s = 0; s < NS; ++s) acc[s] = v16i{0};
-    fetch(0);
-    stash(0);
+    issue(0, 0);
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __syncthreads();
-    for (int kc = 0; kc < MK / KS; ++kc) {
-        const int buf = kc & 1;
-        if (kc + 1 < MK / KS) fetch(kc + 1);
+    for (int s = 0; s < MK / KS; ++s) {
+        const int buf = s & 1;
+        if (s + 1 < MK / KS) issue(s + 1, buf ^ 1);   // buf ^ 1's last readers all passed the previous barrier
         const int8_t* st = lds + buf * STAGE;
-        v4i bv[D];
 #pragma unroll
-        for (int j = 0; j < D; ++j) bv[j] = *(const v4i*)(st + (D + j) * PLANE + (wp + r) * KS + 16 * h);
+        for (int pp = 0; pp < 2; ++pp) {
+            v4i bv[D];
 #pragma unroll
-        for (int i = 0; i < D; ++i) {
-            const v4i av = *(const v4i*)(st + i * PLANE + (wm + r) * KS + 16 * h);
+            for (int j = 0; j < D; ++j)
+                bv[j] = *(const v4i*)(st + (D + j) * PLANE + pp * PANEL + (wp + r) * 32 + 16 * h);
 #pragma unroll
-            for (int j = 0; j < D; ++j) acc[i + j] = __builtin_amdgcn_mfma_i32_32x32x32_i8(av, bv[j], acc[i + j], 0, 0, 0);
+            for (int i = 0; i < D; ++i) {
+                const v4i av = *(const v4i*)(st + i * PLANE + pp * PANEL + (wm + r) * 32 + 16 * h);
+#pragma unroll
+                for (int j = 0; j < D; ++j)
+                    acc[i + j] = __builtin_amdgcn_mfma_i32_32x32x32_i8(av, bv[j], acc[i + j], 0, 0, 0);
+            }
         }
-        if (kc + 1 < MK / KS) stash(buf ^ 1);   // readers of buf ^ 1 all passed the previous barrier
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // this wave's DMA into buf ^ 1 has landed
         __syncthreads();
     }
     mfma_epilogue<D>(a, acc, l, mb + wm, (uint32_t)(pb + wp), r, h);
