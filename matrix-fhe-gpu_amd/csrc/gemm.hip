@@ -148,6 +148,120 @@ __global__ __launch_bounds__(NTH) void cgemm_kernel(CGemmArgs a) {
     }
 }
 
+// ---------------- FP64 MFMA complex GEMM (W-DFT, XY transforms) ----------------
+//
+// C = A B over complex doubles as four real products on v_mfma_f64_16x16x4_f64:
+//   Cr += Ar Br + (-Ai) Bi,  Ci += Ar Bi + Ai Br.
+// A workgroup computes a 64 x 64 tile of C (four 32 x 32 wave tiles of 2 x 2 MFMA blocks); each
+// 16-deep K stage of A and B goes global -> registers -> LDS (split into re / im planes) one stage
+// ahead of the MFMAs that read it.  Products are exact-rounded f64 FMAs, so the sum differs from the
+// oracle's mul-then-add order by ~1e-16 relative per term -- the FP_TOL parity of the VALU kernel
+// above, which stays selectable (MFHE_OPT_CGEMM_MFMA = 0).
+// Fragment maps (f64 16x16x4): A lane l = A[l&15][k=l>>4], B lane l = B[k=l>>4][l&15],
+// C/D reg j of lane l = C[(l>>4) + 4j][l&15].
+typedef double v4d __attribute__((ext_vector_type(4)));
+constexpr int CKT = 16;          // K per LDS stage
+constexpr int CAP = CKT + 1;     // A plane row pitch (doubles): spreads a fragment's 16 rows over the banks
+
+__global__ __launch_bounds__(NTH, 2) void cgemm_mfma_kernel(CGemmArgs a) {
+    __shared__ double Ar[2][TM * CAP], Ai[2][TM * CAP];   // [row][k]
+    __shared__ double Br[2][CKT * TP], Bi[2][CKT * TP];   // [k][col]
+    const int bt = blockIdx.z;
+    const int m0 = blockIdx.y * TM;
+    const uint32_t p0 = blockIdx.x * TP;
+    const int t = threadIdx.x, lane = t & 63, w = t >> 6;
+    const int wm = (w >> 1) * 32, wp = (w & 1) * 32, r = lane & 15, kq = lane >> 4;
+    const double2* A = a.A + (uint64_t)bt * a.aB;
+    const double2* B = a.B + (uint64_t)bt * a.bB;
+    double2 ra[(TM * CKT) / NTH], rb[(CKT * TP) / NTH];
+    auto load = [&](int k0) {
+#pragma unroll
+        for (int e = 0; e < (TM * CKT) / NTH; ++e) {   // A stage 64 x 16, 16 consecutive k per row
+            const int idx = t + e * NTH, m = m0 + (idx >> 4), k = k0 + (idx & 15);
+            ra[e] = (m < a.M && k < a.K) ? A[(uint64_t)m * a.K + k] : make_double2(0, 0);
+        }
+#pragma unroll
+        for (int e = 0; e < (CKT * TP) / NTH; ++e) {   // B stage 16 x 64, coalesced along p
+            const int idx = t + e * NTH, k = k0 + (idx >> 6);
+            const uint32_t p = p0 + (idx & 63);
+            rb[e] = (k < a.K && p < a.P) ? B[b_off(k, p, a.sbK, a.sbY, a.log_n)] : make_double2(0, 0);
+        }
+    };
+    auto store = [&](int buf) {
+#pragma unroll
+        for (int e = 0; e < (TM * CKT) / NTH; ++e) {
+            const int idx = t + e * NTH, o = (idx >> 4) * CAP + (idx & 15);
+            Ar[buf][o] = ra[e].x;
+            Ai[buf][o] = ra[e].y;
+        }
+#pragma unroll
+        for (int e = 0; e < (CKT * TP) / NTH; ++e) {
+            const int idx = t + e * NTH;
+            Br[buf][idx] = rb[e].x;
+            Bi[buf][idx] = rb[e].y;
+        }
+    };
+    v4d cr[2][2], ci[2][2];
+#pragma unroll
+    for (int i = 0; i < 2; ++i)
+#pragma unroll
+        for (int j = 0; j < 2; ++j) cr[i][j] = ci[i][j] = v4d{0, 0, 0, 0};
+    const int nk = (a.K + CKT - 1) / CKT;
+    load(0);
+    store(0);
+    __syncthreads();
+    for (int kt = 0; kt < nk; ++kt) {
+        const int buf = kt & 1;
+        if (kt + 1 < nk) load((kt + 1) * CKT);
+#pragma unroll
+        for (int ks = 0; ks < CKT / 4; ++ks) {
+            const int k = ks * 4 + kq;
+            double ar[2], ai[2], nai[2], br[2], bi[2];
+#pragma unroll
+            for (int i = 0; i < 2; ++i) {
+                ar[i] = Ar[buf][(wm + 16 * i + r) * CAP + k];
+                ai[i] = Ai[buf][(wm + 16 * i + r) * CAP + k];
+                nai[i] = -ai[i];
+            }
+#pragma unroll
+            for (int j = 0; j < 2; ++j) {
+                br[j] = Br[buf][k * TP + wp + 16 * j + r];
+                bi[j] = Bi[buf][k * TP + wp + 16 * j + r];
+            }
+            // first terms of all eight accumulators, then the second terms: no back-to-back dependence
+#pragma unroll
+            for (int i = 0; i < 2; ++i)
+#pragma unroll
+                for (int j = 0; j < 2; ++j) {
+                    cr[i][j] = __builtin_amdgcn_mfma_f64_16x16x4f64(ar[i], br[j], cr[i][j], 0, 0, 0);
+                    ci[i][j] = __builtin_amdgcn_mfma_f64_16x16x4f64(ar[i], bi[j], ci[i][j], 0, 0, 0);
+                }
+#pragma unroll
+            for (int i = 0; i < 2; ++i)
+#pragma unroll
+                for (int j = 0; j < 2; ++j) {
+                    cr[i][j] = __builtin_amdgcn_mfma_f64_16x16x4f64(nai[i], bi[j], cr[i][j], 0, 0, 0);
+                    ci[i][j] = __builtin_amdgcn_mfma_f64_16x16x4f64(ai[i], br[j], ci[i][j], 0, 0, 0);
+                }
+        }
+        if (kt + 1 < nk) store(buf ^ 1);
+        __syncthreads();
+    }
+    double2* C = a.C + (uint64_t)bt * a.cB;
+#pragma unroll
+    for (int i = 0; i < 2; ++i)
+#pragma unroll
+        for (int j = 0; j < 2; ++j) {
+            const uint32_t p = p0 + wp + 16 * j + r;
+            if (p >= a.P) continue;
+#pragma unroll
+            for (int g = 0; g < 4; ++g) {
+                const int m = m0 + wm + 16 * i + kq + 4 * g;
+                if (m < a.M) C[b_off(m, p, a.scM, a.scY, a.log_n)] = make_double2(cr[i][j][g], ci[i][j][g]);
+            }
+        }
+}
+
 // ---------------- i8 MFMA modular GEMM (W-CRT, M = K = 512) ----------------
 //
 // Exact integer product through v_mfma_i32_32x32x32_i8: every operand x < q < 2^(8D-1) is written in
@@ -423,8 +537,13 @@ int launch_mod_gemm(const ModGemmArgs& a, int L, hipStream_t s) {
 
 int launch_cgemm(const CGemmArgs& a, int batch, hipStream_t s) {
     dim3 grid((a.P + TP - 1) / TP, (a.M + TM - 1) / TM, batch);
-    hipLaunchKernelGGL(cgemm_kernel, grid, dim3(NTH), 0, s, a);
-    MFHE_CHECK_LAUNCH("cgemm_kernel");
+    if (a.mfma) {
+        hipLaunchKernelGGL(cgemm_mfma_kernel, grid, dim3(NTH), 0, s, a);
+        MFHE_CHECK_LAUNCH("cgemm_mfma_kernel");
+    } else {
+        hipLaunchKernelGGL(cgemm_kernel, grid, dim3(NTH), 0, s, a);
+        MFHE_CHECK_LAUNCH("cgemm_kernel");
+    }
     return MFHE_OK;
 }
 

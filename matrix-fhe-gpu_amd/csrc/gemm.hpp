@@ -52,6 +52,7 @@ struct CGemmArgs {
     uint64_t sbK, sbY, scM, scY;
     int M, K, log_n;
     uint32_t P;
+    bool mfma = true;      // f64 MFMA kernel; false = VALU mul-then-add kernel (oracle term order)
 };
 
 int launch_mod_gemm(const ModGemmArgs& a, int L, hipStream_t s);

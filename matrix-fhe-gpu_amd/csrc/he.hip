@@ -369,6 +369,7 @@ static int wcrt_gemm(mfhe_ctx* c, const uint64_t* A, const uint64_t* B, bool b_p
 static int wdft(const mfhe_ctx* c, const double2* A, const double2* in, double2* out, hipStream_t s) {
     const Geo2 g = geo(c);
     CGemmArgs a;
+    a.mfma = c->cgemm_mfma != 0;
     a.A = A; a.B = in; a.C = out;
     a.aB = a.bB = a.cB = 0;
     a.M = a.K = 512;
@@ -383,6 +384,7 @@ static int xy3(const mfhe_ctx* c, const double2* A, const double2* in, const dou
                size_t lanes, hipStream_t s) {
     const Geo2 g = geo(c);
     CGemmArgs a;
+    a.mfma = c->cgemm_mfma != 0;
     a.M = a.K = (int)g.n;
     a.P = (uint32_t)g.n;
     a.log_n = g.logn;

@@ -84,6 +84,7 @@ struct mfhe_ctx {
     std::vector<int> wDl;        // digits limb l needs (<= wD): its higher planes are all zero
     double* d_wepi = nullptr;    // [L][8] FP64 epilogue constants (gemm.hip GemmEpiF), null: integer epilogue
     int wcrt_mfma = 1;           // MFHE_OPT_WCRT_MFMA
+    int cgemm_mfma = 1;          // MFHE_OPT_CGEMM_MFMA
     void* gemm_ws = nullptr;     // B digit planes for the MFMA GEMM, grown on demand
     size_t gemm_ws_bytes = 0;
     size_t fused_bytes = 0;

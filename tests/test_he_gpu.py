@@ -110,9 +110,48 @@ def test_wcrt_centered_matches_reference_semantics(mfhe, orc, small):
     np.testing.assert_array_equal(rt1.cpu().numpy(), coeff)
 
 
-def test_wdft_and_xy_transforms_vs_oracle(mfhe, orc, small):
-    import torch
+@pytest.mark.parametrize("cgemm", [1, 0])
+def test_wdft_and_xy_transforms_vs_oracle(mfhe, orc, small, cgemm):
+    """W-DFT / XY transforms on the f64 MFMA complex GEMM (1, default) and the VALU kernel (0)."""
     n, ctx, h = small
+    ctx.set_option(mfhe.OPT_CGEMM_MFMA, cgemm)
+    try:
+        _wdft_and_xy_transforms(mfhe, orc, n, ctx)
+    finally:
+        ctx.set_option(mfhe.OPT_CGEMM_MFMA, 1)
+
+
+@pytest.mark.parametrize("n", [4, 16, 64])
+def test_cgemm_mfma_matches_valu(mfhe, n):
+    """f64 MFMA complex GEMM (gemm.hip cgemm_mfma_kernel) vs the VALU kernel at tile-ragged and full sizes:
+    XY-IDFT / XY-DFT (M = K = P = n per lane) and W-DFT / W-IDFT (M = K = 512, P = n^2), 1e-12 relative."""
+    import torch
+    ctx = mfhe.Context(RNS[:2], n.bit_length() - 1, CONV)
+    n2 = n * n
+    rng = np.random.default_rng(n)
+    z = (rng.standard_normal(512 * n2) + 1j * rng.standard_normal(512 * n2)).astype(np.complex128)
+    zt = torch.from_numpy(z.view(np.float64).copy()).cuda()
+    outs = {}
+    for mode in (1, 0):
+        ctx.set_option(mfhe.OPT_CGEMM_MFMA, mode)
+        assert ctx.get_option(mfhe.OPT_CGEMM_MFMA) == mode
+        res = []
+        for fn in (ctx.xy_idft, ctx.xy_dft):
+            o = torch.empty_like(zt)
+            fn(zt, o, 512)
+            res.append(o)
+        for fn in (ctx.wdft_fwd, ctx.wdft_inv):
+            o = torch.empty_like(zt)
+            fn(zt, o)
+            res.append(o)
+        torch.cuda.synchronize()
+        outs[mode] = [r.cpu().numpy() for r in res]
+    for a, b in zip(outs[1], outs[0]):
+        assert np.max(np.abs(a - b)) <= 1e-12 * np.max(np.abs(b))
+
+
+def _wdft_and_xy_transforms(mfhe, orc, n, ctx):
+    import torch
     n2 = n * n
     rng = np.random.default_rng(2)
     z = (rng.standard_normal(512 * n2) + 1j * rng.standard_normal(512 * n2)).astype(np.complex128)
@@ -251,7 +290,9 @@ def test_encode_stages_and_decode_vs_oracle(mfhe, orc, small):
     """encode_to_wntt_eval stage by stage: FP64 XY-IDFT and W-IDFT within tolerance of the oracle; the
     integer stage (quantize + RNS split + W-CRT, batched_encoder.cu:125-152 + HE.cu:716-747) bit-exact
     from identical doubles.  (End to end, one FP64 rounding difference before llround changes one
-    coefficient, which the W-CRT spreads over a whole column -- tolerance parity only)"""
+    coefficient, which the W-CRT spreads over a whole column -- tolerance parity only, SURVEY.md §8c.
+    The default f64 MFMA GEMM sums in its own order, so its encode is checked bit-exact against the
+    integer stage on its own doubles; the oracle-order VALU GEMM is checked against the oracle.)"""
     import torch
     n, ctx, h = small
     n2 = n * n
@@ -296,11 +337,24 @@ def test_encode_stages_and_decode_vs_oracle(mfhe, orc, small):
         ctx.poly_to_matrix(ev, out)
         torch.cuda.synchronize()
         np.testing.assert_array_equal(mfhe.to_host_u64(out), ref)
-    # full device encode: integer outputs equal except in columns where llround saw a different double
+    # full device encode == the integer stage run on the device's own W-IDFT doubles, bit-exact
     gre = torch.empty(words, dtype=torch.int64, device="cuda")
     gim = torch.empty_like(gre)
     ctx.encode(mt, gre, gim)
-    torch.cuda.synchronize()
+    for part, got in ((0, gre), (1, gim)):
+        ctx.rns_decompose(gwc[part:], cre, 512, n2, in_stride=2)
+        ctx.wcrt_fwd(cre, ev)
+        ctx.poly_to_matrix(ev, out)
+        torch.cuda.synchronize()
+        np.testing.assert_array_equal(mfhe.to_host_u64(out), mfhe.to_host_u64(got))
+    # vs the oracle: with the VALU GEMM (the oracle's mul-then-add term order) the integer outputs are
+    # equal except in at most 2 columns where llround saw a different double
+    ctx.set_option(mfhe.OPT_CGEMM_MFMA, 0)
+    try:
+        ctx.encode(mt, gre, gim)
+        torch.cuda.synchronize()
+    finally:
+        ctx.set_option(mfhe.OPT_CGEMM_MFMA, 1)
     diff_cols = np.any((mfhe.to_host_u64(gre) != ore).reshape(512, 11, n2), axis=(0, 1))
     assert diff_cols.sum() <= 2
     # decode of the oracle's encoding vs the oracle's decode, and the reference 1e-3 bound
