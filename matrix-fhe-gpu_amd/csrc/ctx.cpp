@@ -183,6 +183,13 @@ static int build_crt(mfhe_ctx* c, int min_words) {
     return MFHE_OK;
 }
 
+// balanced base-256 digits every x in [0, q) needs: the smallest d with q - 1 <= 127 (256^d - 1) / 255
+static int wcrt_digits(uint64_t q) {
+    int d = 1;
+    for (hm::u128 top = 127; d < 9 && (hm::u128)(q - 1) > top; ++d) top = top * 256 + 127;
+    return d;
+}
+
 // W-axis tables: init_wntt_tables (HE.cu:237-273), init_wdft_tables (HE.cu:275-310),
 // Encoder::init_complex_matrices (encoder.cu:425-444).
 static int build_wcrt(mfhe_ctx* c) {
@@ -247,13 +254,10 @@ static int build_wcrt(mfhe_ctx* c) {
         return rc;
     // i8 MFMA operand planes (gemm.hip): D balanced base-256 digits of every V / V^-1 entry, and
     // 256^s mod q for the epilogue.  Needs 2^27 < q (|acc_s| < q) and q < 2^59 (D <= 8).
-    int bits = 0;
     bool big = true;
-    for (uint64_t q : c->moduli) {
-        bits = std::max(bits, 64 - __builtin_clzll(q));
-        big = big && q > (1ull << 27);
-    }
-    const int D = std::max(5, (bits + 1 + 7) / 8);
+    for (uint64_t q : c->moduli) big = big && q > (1ull << 27);
+    int D = 5;
+    for (uint64_t q : c->moduli) D = std::max(D, wcrt_digits(q));
     if (big && D <= 8) {
         const size_t plane = (size_t)PHI * PHI;
         std::vector<int8_t> vd((size_t)L * D * plane), vid((size_t)L * D * plane);
@@ -279,12 +283,11 @@ static int build_wcrt(mfhe_ctx* c) {
         if ((rc = upload(c, &c->d_wVdig, vd)) || (rc = upload(c, &c->d_wVidig, vid)) || (rc = upload(c, &c->d_wrtab, rt)))
             return rc;
         c->wD = D;
-        // per-limb digit count: a value < q < 2^(8 d - 1) has zero balanced digits from d on, so limb l's
+        // per-limb digit count: every value in [0, q) has zero balanced digits from d_l on, so limb l's
         // products with those planes vanish and its GEMM runs at d_l^2 instead of D^2 MFMAs
         c->wDl.resize(L);
         for (int l = 0; l < L; ++l) {
-            const int b = 64 - __builtin_clzll(c->moduli[l]);
-            c->wDl[l] = std::min(D, std::max(1, (b + 1 + 7) / 8));
+            c->wDl[l] = std::min(D, wcrt_digits(c->moduli[l]));
         }
         // FP64 epilogue constants (every q < 2^50): q, 1/q and centred 2^32, 2^64, 2^96 mod q
         if (c->f64_ok) {
@@ -300,6 +303,35 @@ static int build_wcrt(mfhe_ctx* c) {
                 ep[(size_t)l * 8 + 4] = centred(p96, q);
             }
             if ((rc = upload(c, &c->d_wepi, ep))) return rc;
+            // factored forward (gemm.hip, 771 = 3 x 257): zeta = eta^3 of order 257, omega = eta^257 of order 3
+            if (D <= 6) {
+                constexpr int FK = 256;
+                std::vector<int8_t> zd((size_t)L * D * FK * FK);
+                std::vector<double> fo((size_t)L * 16, 0.0);
+                for (int l = 0; l < L; ++l) {
+                    const uint64_t q = c->moduli[l], eta = hm::find_eta771(q);
+                    const uint64_t zeta = hm::powmod(eta, 3, q), omega = hm::powmod(eta, 257, q);
+                    int8_t d[8];
+                    for (int i = 0; i < FK; ++i) {
+                        const uint64_t zi = hm::powmod(zeta, (uint64_t)i + 1, q);
+                        uint64_t cur = zi;
+                        for (int k = 0; k < FK; ++k, cur = hm::mulmod(cur, zi, q)) {
+                            balanced_digits(cur, D, d);
+                            const size_t o = ((size_t)(k >> 5) * FK + i) * 32 + (k & 31);
+                            for (int j = 0; j < D; ++j) zd[((size_t)l * D + j) * FK * FK + o] = d[j];
+                        }
+                    }
+                    fo[(size_t)l * 16 + 0] = (double)q;
+                    fo[(size_t)l * 16 + 1] = 1.0 / (double)q;
+                    for (int ap = 0; ap < 2; ++ap)
+                        for (int r1 = 0; r1 < 3; ++r1) {
+                            fo[(size_t)l * 16 + 2 + 3 * ap + r1] = centred(hm::powmod(omega, (uint64_t)(ap + 1) * r1, q), q);
+                            fo[(size_t)l * 16 + 8 + 3 * ap + r1] =
+                                centred(hm::powmod(omega, (uint64_t)(ap + 1) * ((r1 + 2) % 3), q), q);
+                        }
+                }
+                if ((rc = upload(c, &c->d_wZdig, zd)) || (rc = upload(c, &c->d_wfold, fo))) return rc;
+            }
         }
     }
     return MFHE_OK;
@@ -530,7 +562,7 @@ extern "C" int mfhe_ctx_set_option(mfhe_ctx* c, int opt, int64_t v) {
             c->ntt_fused_lag = (int)v;
             return MFHE_OK;
         case MFHE_OPT_WCRT_MFMA:
-            if (v < 0 || v > 2) return set_error(MFHE_EINVAL, "wcrt mfma must be 0, 1 or 2");
+            if (v < 0 || v > 3) return set_error(MFHE_EINVAL, "wcrt mfma must be 0, 1, 2 or 3");
             c->wcrt_mfma = (int)v;
             return MFHE_OK;
         case MFHE_OPT_CGEMM_MFMA:

@@ -280,6 +280,15 @@ using v16i = int __attribute__((ext_vector_type(16)));
 // columns) is 2 KiB of contiguous memory: every fragment load (16 B per lane, lanes over rows and k halves)
 // and every digitize store below is a fully coalesced sweep.
 //
+// Balanced base-256 digits by offset: x = sum d_i 256^i with d_i in [-128, 127] iff
+// y = x + 128 (256^D - 1) / 255 = x + 0x8080..80 has bytes d_i + 128, so d_i = byte_i(y) ^ 0x80 as an i8.
+// Valid for -0x80..80 <= x <= 0x7F..7F (D bytes); the fold kernel's |x| <= q/2 + 1 is well inside.
+template <int D>
+__device__ __forceinline__ uint64_t balanced_bytes(double v) {   // v integral, |v| < 2^51
+    constexpr double kMagic = 6755399441055744.0;                 // 1.5 * 2^52: bits(v + M) - bits(M) = v
+    constexpr uint64_t kOff = 0x8080808080808080ull >> (64 - 8 * D);
+    return (uint64_t)__double_as_longlong(v + kMagic) - ((uint64_t)__double_as_longlong(kMagic) - kOff);
+}
 // one thread: column p (of Ppad; zero past P), one 32-k panel; B (k, p) via the (sbK, sbY, log_n) map
 template <int D>
 __global__ __launch_bounds__(256) void mfma_digitize_kernel(const uint64_t* __restrict__ B, uint64_t bL,
@@ -314,13 +323,104 @@ __global__ __launch_bounds__(256) void mfma_digitize_kernel(const uint64_t* __re
     }
 }
 
-// C = sum_s acc_s * 256^s mod q for the 32 x 32 wave tile at (m0, p0) of limb l (lane = (r, h))
+// ---- factored forward W-CRT (every q < 2^50) ----
+// The 512 evaluation points are eta^e for the units e of Z_771 in the order e = 257 a + 3 b (a = 1, 2;
+// b = 1..256; HE.cu:72-105, k_wntt_exp).  With omega = eta^257 (order 3) and zeta = eta^3 (order 257),
+// x_w^r = omega^(a (r mod 3)) zeta^(b (r mod 257)), and since r < 512 < 771 each r2 = r mod 257 takes at
+// most two r (r2 and r2 + 257):
+//   out[a][b] = F_a[0] + sum_{k < 256} zeta^(b (k + 1)) F_a[k + 1],
+//   F_a[r2]   = omega^(a (r2 mod 3)) in[r2] + omega^(a ((r2 + 2) mod 3)) in[r2 + 257]   (second term if < 512).
+// That is a 256 x 256 GEMM over 2 P columns (a, p) instead of 512 x 512 over P: half the MACs, and the
+// same linear map mod q, so bit-exact.  This kernel forms F_a (two FP64 modmuls per term), writes the
+// digit planes of F_a[1..256] as the B operand ([L][D][8 panels][2 Ppad][32], column a' Ppad + p for
+// a = a' + 1) and F_a[0] to d0[L][2][Ppad] for the GEMM epilogue.
+// fold[l][16] = q, 1/q, omega^(a r1) [a'][r1], omega^(a ((r1 + 2) mod 3)) [a'][r1], all centred.
+constexpr int FK = 256;   // K (and M) of the factored GEMM
+
+// One thread: column p, one half (16 k) of a 32-k panel, both a; lane pairs share a column, so each
+// 16-byte store completes a 1 KiB contiguous run per wave.  The digits need any representative of F_a mod q
+// within the limb's digit range, so F_a is only reduced to the centred (-q/2, q/2] and split by the offset
+// rule (balanced_bytes).
 template <int D>
+__global__ __launch_bounds__(256) void mfma_digitize_fold_kernel(const uint64_t* __restrict__ B, uint64_t bL,
+                                                                 uint64_t sbK, uint64_t sbY, int log_n, uint32_t P,
+                                                                 uint32_t Ppad, const double* __restrict__ fold,
+                                                                 int8_t* __restrict__ out, uint64_t* __restrict__ d0) {
+    const uint32_t p = blockIdx.x * 128 + (threadIdx.x >> 1);
+    const int hf = threadIdx.x & 1;
+    const int kc = blockIdx.y;   // panel: r2 = 32 kc + 16 hf + 1 .. 32 kc + 16 hf + 16
+    const int l = blockIdx.z;
+    if (p >= Ppad) return;
+    const double* fo = fold + (uint64_t)l * 16;
+    LimbConst lc;
+    lc.qf = fo[0];
+    lc.qinv = fo[1];
+    const ArithF64 ar(lc);
+    double c1[2][3], c2[2][3];
+#pragma unroll
+    for (int ap = 0; ap < 2; ++ap)
+#pragma unroll
+        for (int r1 = 0; r1 < 3; ++r1) {
+            c1[ap][r1] = fo[2 + 3 * ap + r1];
+            c2[ap][r1] = fo[8 + 3 * ap + r1];
+        }
+    const uint64_t* Bl = B + (uint64_t)l * bL;
+    const uint64_t col = (uint64_t)(p >> log_n) * sbY + (p & ((1u << log_n) - 1));
+    const bool live = p < P;
+    auto in = [&](int r) { return live ? ArithF64::from_u64(Bl[(uint64_t)r * sbK + col]) : 0.0; };
+    uint32_t pk[2][D][4];
+#pragma unroll
+    for (int ap = 0; ap < 2; ++ap)
+#pragma unroll
+        for (int i = 0; i < D; ++i)
+#pragma unroll
+            for (int c = 0; c < 4; ++c) pk[ap][i][c] = 0;
+    const int rb = kc * 32 + hf * 16 + 1;
+    int r1 = rb % 3;
+#pragma unroll
+    for (int kk = 0; kk < 16; ++kk) {
+        const int r2 = rb + kk;
+        const double x1 = in(r2), x2 = r2 + 257 < 512 ? in(r2 + 257) : 0.0;
+#pragma unroll
+        for (int ap = 0; ap < 2; ++ap) {
+            const double w1 = r1 == 0 ? c1[ap][0] : (r1 == 1 ? c1[ap][1] : c1[ap][2]);
+            const double w2 = r1 == 0 ? c2[ap][0] : (r1 == 1 ? c2[ap][1] : c2[ap][2]);
+            const double v = ar.reduce(ar.mulmod(x1, w1) + ar.mulmod(x2, w2));   // |v| <= q/2 + eps
+            const uint64_t y = balanced_bytes<D>(v);
+            const uint32_t lo = (uint32_t)y, hi = (uint32_t)(y >> 32);
+#pragma unroll
+            for (int i = 0; i < D; ++i) {
+                const uint32_t b = i < 4 ? (lo >> (8 * i)) & 255u : (hi >> (8 * (i - 4))) & 255u;
+                pk[ap][i][kk >> 2] |= b << (8 * (kk & 3));
+            }
+        }
+        r1 = r1 == 2 ? 0 : r1 + 1;
+    }
+    if (kc == 0 && hf == 0) {
+        const double x1 = in(0), x2 = in(257);
+#pragma unroll
+        for (int ap = 0; ap < 2; ++ap)
+            d0[((uint64_t)l * 2 + ap) * Ppad + p] = ar.canon(ar.mulmod(x1, c1[ap][0]) + ar.mulmod(x2, c2[ap][0]));
+    }
+#pragma unroll
+    for (int ap = 0; ap < 2; ++ap)
+#pragma unroll
+        for (int i = 0; i < D; ++i) {
+            int8_t* o = out + ((((uint64_t)l * D + i) * (FK / 32) + kc) * 2 * Ppad + (uint64_t)ap * Ppad + p) * 32 + hf * 16;
+            const uint32_t* w = pk[ap][i];
+            *(v4i*)o = v4i{(int)(w[0] ^ 0x80808080u), (int)(w[1] ^ 0x80808080u), (int)(w[2] ^ 0x80808080u),
+                           (int)(w[3] ^ 0x80808080u)};
+        }
+}
+
+// C = sum_s acc_s * 256^s mod q for the 32 x 32 wave tile at (m0, p0) of limb l (lane = (r, h)).
+// FAC: factored forward -- column p0 + r is (a', p) = divmod(., Ppad), output row a' * 256 + row, plus d0.
+template <int D, bool FAC = false>
 __device__ __forceinline__ void mfma_epilogue(const ModGemmArgs& a, const v16i (&acc)[2 * D - 1], int l, int m0,
-                                              uint32_t p0, int r, int h) {
+                                              uint32_t p0, int r, int h, uint32_t Ppad = 0) {
     constexpr int NS = 2 * D - 1;
     uint64_t* Cl = a.C + (uint64_t)l * a.cL;
-    if (a.epi) {
+    if (FAC || a.epi) {
         // FP64 (every q < 2^50): |acc_s| < 2^26, so z_t = acc_2t + 256 acc_2t+1 (< 2^35) and
         // y_u = z_2u + 2^16 z_2u+1 (< 2^51) are exact doubles; C = y_0 + sum_u y_u (2^32u mod q), each
         // product an exact FP64 modmul with a centred constant (|y c / q| < 2^50), then one canonical
@@ -331,18 +431,27 @@ __device__ __forceinline__ void mfma_epilogue(const ModGemmArgs& a, const v16i (
         lc.qinv = ep[1];
         const ArithF64 ar(lc);
         const double c32[3] = {ep[2], ep[3], ep[4]};
-        const uint32_t colf = p0 + r;
+        uint32_t colf = p0 + r;
+        int rbase = 0;
+        double add = 0.0;
+        if (FAC) {
+            const int ap = colf >= Ppad;
+            colf -= ap * Ppad;
+            if (colf >= a.P) return;
+            rbase = ap * FK;
+            add = ArithF64::from_u64(a.d0[((uint64_t)l * 2 + ap) * Ppad + colf]);
+        }
         if (colf >= a.P) return;
         constexpr int NZ = (NS + 1) / 2, NY = (NZ + 1) / 2;
 #pragma unroll
         for (int reg = 0; reg < 16; ++reg) {
-            const int row = m0 + (reg & 3) + 8 * (reg >> 2) + 4 * h;
+            const int row = rbase + m0 + (reg & 3) + 8 * (reg >> 2) + 4 * h;
             double z[NZ];
 #pragma unroll
             for (int t = 0; t < NZ; ++t)
                 z[t] = 2 * t + 1 < NS ? __fma_rn(256.0, (double)acc[2 * t + 1][reg], (double)acc[2 * t][reg])
                                       : (double)acc[2 * t][reg];
-            double v = 0.0;
+            double v = add;
 #pragma unroll
             for (int u = 0; u < NY; ++u) {
                 const double y = 2 * u + 1 < NZ ? __fma_rn(65536.0, z[2 * u + 1], z[2 * u]) : z[2 * u];
@@ -352,6 +461,7 @@ __device__ __forceinline__ void mfma_epilogue(const ModGemmArgs& a, const v16i (
         }
         return;
     }
+    if constexpr (FAC) return;   // factored mode always has the FP64 epilogue (launch_mod_gemm checks)
     const uint64_t q = a.qmu[2 * l], mu = a.qmu[2 * l + 1];
     const uint64_t* rt = a.rtab + (uint64_t)l * NS * 2;
     uint64_t* C = Cl;
@@ -410,8 +520,11 @@ __global__ __launch_bounds__(256, D <= 5 ? 2 : 1) void mod_gemm_mfma_kernel(ModG
 // RAW order for the DMA'd bytes: issuing waves' s_waitcnt vmcnt(0), then the barrier, then the reads.
 typedef __attribute__((address_space(3))) void* lds_ptr_t;
 
-template <int D>
+template <int D, bool FAC>
 __global__ __launch_bounds__(256, D <= 5 ? 2 : 1) void mod_gemm_mfma_lds_kernel(ModGemmArgs a, uint32_t Ppad, int limb0) {
+    // FAC: M = K = 256 and 2 Ppad B columns (factored forward); else M = K = 512 and Ppad columns
+    constexpr int KK = FAC ? FK : MK, AM = FAC ? FK : 512;
+    const uint32_t Pcols = FAC ? 2 * Ppad : Ppad;
     constexpr int NS = 2 * D - 1;
     constexpr int KS = 64;                       // K per stage: two 32-k panels
     constexpr int PANEL = 64 * 32;               // 64 rows x 32 k of one digit plane (bytes)
@@ -426,10 +539,10 @@ __global__ __launch_bounds__(256, D <= 5 ? 2 : 1) void mod_gemm_mfma_lds_kernel(
     // DMA slot li: bytes [16 li, 16 li + 16) of a 2 KiB panel image (row li / 2, k half li & 1)
     const bool ldA = t < 128;
     const int li = t & 127;
-    const uint64_t rows = ldA ? 512 : Ppad;                        // rows of the operand's planes
-    const int8_t* src = (ldA ? a.Adig + (uint64_t)l * a.adL : a.Bdig + (uint64_t)l * a.D * Ppad * MK) +
+    const uint64_t rows = ldA ? AM : Pcols;                        // rows of the operand's planes
+    const int8_t* src = (ldA ? a.Adig + (uint64_t)l * a.adL : a.Bdig + (uint64_t)l * a.D * Pcols * KK) +
                         (uint64_t)(ldA ? mb : pb) * 32 + li * 16;
-    const uint64_t pstride = rows * MK, kstride = rows * 32;      // digit-plane / k-panel strides
+    const uint64_t pstride = rows * KK, kstride = rows * 32;      // digit-plane / k-panel strides
     const int wbase = (ldA ? 0 : D * PLANE) + (li & ~63) * 16;     // this wave's LDS destination base
     auto issue = [&](int s, int buf) {
 #pragma unroll
@@ -446,9 +559,9 @@ __global__ __launch_bounds__(256, D <= 5 ? 2 : 1) void mod_gemm_mfma_lds_kernel(
     issue(0, 0);
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __syncthreads();
-    for (int s = 0; s < MK / KS; ++s) {
+    for (int s = 0; s < KK / KS; ++s) {
         const int buf = s & 1;
-        if (s + 1 < MK / KS) issue(s + 1, buf ^ 1);   // buf ^ 1's last readers all passed the previous barrier
+        if (s + 1 < KK / KS) issue(s + 1, buf ^ 1);   // buf ^ 1's last readers all passed the previous barrier
         const int8_t* st = lds + buf * STAGE;
 #pragma unroll
         for (int pp = 0; pp < 2; ++pp) {
@@ -467,12 +580,12 @@ __global__ __launch_bounds__(256, D <= 5 ? 2 : 1) void mod_gemm_mfma_lds_kernel(
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // this wave's DMA into buf ^ 1 has landed
         __syncthreads();
     }
-    mfma_epilogue<D>(a, acc, l, mb + wm, (uint32_t)(pb + wp), r, h);
+    mfma_epilogue<D, FAC>(a, acc, l, mb + wm, (uint32_t)(pb + wp), r, h, Ppad);
 }
 
 size_t mod_gemm_mfma_ws(uint32_t P, int L, int D) {
     const uint64_t Ppad = ((uint64_t)P + 63) / 64 * 64;
-    return (size_t)L * D * Ppad * MK;
+    return (size_t)L * D * Ppad * MK + (size_t)L * 2 * Ppad * 8;   // digit planes, then the factored d0
 }
 
 void balanced_digits(uint64_t x, int D, int8_t* out) {
@@ -487,7 +600,35 @@ void balanced_digits(uint64_t x, int D, int8_t* out) {
     }
 }
 
+static int launch_factored(const ModGemmArgs& a, int L, hipStream_t s) {
+    const uint32_t Ppad = (a.P + 63) / 64 * 64;
+    ModGemmArgs f = a;
+    f.d0 = (uint64_t*)(a.Bdig + (size_t)L * a.D * Ppad * MK);
+    const dim3 gd((Ppad + 127) / 128, FK / 32, L);
+    if (a.D == 5) hipLaunchKernelGGL(mfma_digitize_fold_kernel<5>, gd, dim3(256), 0, s, a.B, a.bL, a.sbK, a.sbY, a.log_n,
+                                     a.P, Ppad, a.fold, a.Bdig, f.d0);
+    else hipLaunchKernelGGL(mfma_digitize_fold_kernel<6>, gd, dim3(256), 0, s, a.B, a.bL, a.sbK, a.sbY, a.log_n, a.P,
+                            Ppad, a.fold, a.Bdig, f.d0);
+    MFHE_CHECK_LAUNCH("mfma_digitize_fold_kernel");
+    for (int l0 = 0; l0 < L;) {
+        const int d = a.limbD ? std::max(a.limbD[l0], 5) : a.D;
+        int l1 = l0 + 1;
+        while (l1 < L && (a.limbD ? std::max(a.limbD[l1], 5) : a.D) == d) ++l1;
+        const dim3 grid(2 * Ppad / 64, FK / 64, l1 - l0);
+        if (d == 5) hipLaunchKernelGGL((mod_gemm_mfma_lds_kernel<5, true>), grid, dim3(256), 0, s, f, Ppad, l0);
+        else hipLaunchKernelGGL((mod_gemm_mfma_lds_kernel<6, true>), grid, dim3(256), 0, s, f, Ppad, l0);
+        MFHE_CHECK_LAUNCH("mod_gemm_mfma_lds_kernel (factored)");
+        l0 = l1;
+    }
+    return MFHE_OK;
+}
+
 int launch_mod_gemm(const ModGemmArgs& a, int L, hipStream_t s) {
+    if (a.Adig && a.fold) {
+        if (a.M != 512 || a.K != MK || !a.epi || a.D < 5 || a.D > 6 || !a.lds_stage)
+            return set_error(MFHE_EINVAL, "mod_gemm: factored W-CRT needs M = K = 512, the FP64 epilogue and D in {5, 6}");
+        return launch_factored(a, L, s);
+    }
     if (a.Adig && a.M == 512 && a.K == MK) {
         const uint32_t Ppad = (a.P + 63) / 64 * 64;
         const dim3 gd((Ppad + 255) / 256, MK / 32, L);
@@ -514,7 +655,7 @@ int launch_mod_gemm(const ModGemmArgs& a, int L, hipStream_t s) {
             switch (d) {
 #define MFHE_MFMA_CASE(dd)                                                                                    \
     case dd:                                                                                                  \
-        if (a.lds_stage) hipLaunchKernelGGL(mod_gemm_mfma_lds_kernel<dd>, grid, dim3(256), 0, s, a, Ppad, l0); \
+        if (a.lds_stage) hipLaunchKernelGGL((mod_gemm_mfma_lds_kernel<dd, false>), grid, dim3(256), 0, s, a, Ppad, l0); \
         else hipLaunchKernelGGL(mod_gemm_mfma_kernel<dd>, grid, dim3(256), 0, s, a, Ppad, l0);                 \
         break;
                 MFHE_MFMA_CASE(5)

@@ -73,14 +73,13 @@ __device__ __forceinline__ uint64_t splitmix64(uint64_t x) {
     return x ^ (x >> 31);
 }
 
-// gaussian_noise_kernel HE.cu:581-627: one centred sample per [w][y][x], same integer in every limb
+// gaussian_noise_kernel HE.cu:581-627: one centred sample per [w][y][x], same integer in every limb.
+// One thread per sample (the reference draws it once per limb), written to all L limbs.
 __global__ void gaussian_kernel(uint64_t* e, const uint64_t* qmu, int L, int log_n, uint64_t total) {
     const uint64_t idx = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x;
     if (idx >= total) return;
-    const uint64_t n2 = 1ull << (2 * log_n), single = (uint64_t)L * n2;
-    const uint64_t w = idx / single, off = idx % single;
-    const int limb = (int)(off / n2);
-    const uint64_t pos = off % n2;
+    const uint64_t n2 = 1ull << (2 * log_n);
+    const uint64_t w = idx >> (2 * log_n), pos = idx & (n2 - 1);
     const uint64_t r1 = splitmix64(0xD6E8FEB86659FD93ULL ^ (w * n2 + pos));
     const uint64_t r2 = splitmix64(r1);
     const double inv53 = 1.0 / 9007199254740992.0;
@@ -89,8 +88,11 @@ __global__ void gaussian_kernel(uint64_t* e, const uint64_t* qmu, int L, int log
     const double mag = 3.2 * sqrt(-2.0 * log(u1));
     const double z = mag * cos(6.283185307179586 * u2);
     const long long nz = llround(z);
-    const uint64_t q = qmu[2 * limb];
-    e[idx] = (nz >= 0) ? (uint64_t)nz : q - (uint64_t)(-nz);
+    uint64_t* out = e + w * L * n2 + pos;
+    for (int limb = 0; limb < L; ++limb) {
+        const uint64_t q = qmu[2 * limb];
+        out[(uint64_t)limb * n2] = (nz >= 0) ? (uint64_t)nz : q - (uint64_t)(-nz);
+    }
 }
 
 // ---------------- ring ops (poly-major [phi*n][L][n]) ----------------
@@ -334,6 +336,12 @@ static int use_mfma(mfhe_ctx* c, ModGemmArgs& a, const uint64_t* A, int L) {
     a.limbD = (a.aL && (int)c->wDl.size() == L) ? c->wDl.data() : nullptr;
     a.epi = c->d_wepi;
     a.lds_stage = c->wcrt_mfma != 2;
+    // mode 1: the forward transform of a per-limb V runs factored (half the MACs, gemm.hip)
+    if (c->wcrt_mfma == 1 && A == c->d_wV && a.aL && c->d_wZdig && a.epi) {
+        a.Adig = c->d_wZdig;
+        a.adL = (uint64_t)c->wD * 256 * 256;
+        a.fold = c->d_wfold;
+    }
     return MFHE_OK;
 }
 
@@ -489,7 +497,7 @@ static int encrypt_impl(mfhe_ctx* c, const uint64_t* m_re, const uint64_t* m_im,
     MFHE_HIP(hipMemcpyAsync(ant, aev, W * 8, hipMemcpyDeviceToDevice, s));
     RC(mfhe_ntt_fwd(c, ant, 512 * g.n, 0, g.L, (mfhe_stream_t)s));
     // e: identical for re and im (seed depends only on the coefficient, HE.cu:605-608)
-    hipLaunchKernelGGL(gaussian_kernel, g1(W), dim3(256), 0, s, ep, c->d_rns_mu, g.L, g.logn, W);
+    hipLaunchKernelGGL(gaussian_kernel, g1(W / g.L), dim3(256), 0, s, ep, c->d_rns_mu, g.L, g.logn, W / g.L);
     MFHE_CHECK_LAUNCH("gaussian_kernel");
     RC(wcrt_gemm(c, c->d_wV, ep, false, eev, WOut::Poly, false, s));
     // t = INTT(a_ntt * s)  (reuse ep as t)

@@ -83,6 +83,8 @@ struct mfhe_ctx {
     int wD = 0;                  // 0: no MFMA tables (some q <= 2^27); else the plane stride (max digits)
     std::vector<int> wDl;        // digits limb l needs (<= wD): its higher planes are all zero
     double* d_wepi = nullptr;    // [L][8] FP64 epilogue constants (gemm.hip GemmEpiF), null: integer epilogue
+    int8_t* d_wZdig = nullptr;   // [L][wD][256][256] digits of Z[i][k] = zeta^((i+1)(k+1)) (factored forward W-CRT)
+    double* d_wfold = nullptr;   // [L][16] factored forward fold constants (gemm.hip mfma_digitize_fold_kernel)
     int wcrt_mfma = 1;           // MFHE_OPT_WCRT_MFMA
     int cgemm_mfma = 1;          // MFHE_OPT_CGEMM_MFMA
     void* gemm_ws = nullptr;     // B digit planes for the MFMA GEMM, grown on demand

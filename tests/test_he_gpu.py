@@ -441,7 +441,8 @@ def test_kat7_kat8_encrypt_decrypt_reference_geometry(mfhe, pattern, tol):
 @pytest.mark.parametrize("n,L", [(8, 11), (64, 11), (4, 2), (16, 1)])
 def test_wcrt_mfma_matches_valu_and_oracle(mfhe, orc, n, L):
     """W-CRT GEMM on i8 MFMA (digit-split exact product, gemm.hip) == the u128 VALU kernel == oracle,
-    all three layouts (matrix->poly, poly->matrix, vector), bit-exact."""
+    all three layouts (matrix->poly, poly->matrix, vector), bit-exact.  Modes: 1 = LDS-staged with the
+    forward factored through 771 = 3 x 257 (default), 3 = LDS-staged dense, 2 = global fragments, 0 = VALU."""
     import torch
     log_n = n.bit_length() - 1
     ctx = mfhe.Context(RNS[:L], log_n, CONV)
@@ -449,7 +450,7 @@ def test_wcrt_mfma_matches_valu_and_oracle(mfhe, orc, n, L):
     rng = np.random.default_rng(n * 100 + L)
     x = _rand_mat(rng, n, L)
     outs = {}
-    for mf in (1, 2, 0):
+    for mf in (1, 3, 2, 0):
         ctx.set_option(mfhe.OPT_WCRT_MFMA, mf)
         d = _dev(mfhe, x)
         f = torch.empty_like(d)
@@ -464,7 +465,7 @@ def test_wcrt_mfma_matches_valu_and_oracle(mfhe, orc, n, L):
         np.testing.assert_array_equal(outs[mf][1], x)
         rng = np.random.default_rng(n * 100 + L)   # same vector input for both runs
         _rand_mat(rng, n, L)
-    for mf in (1, 2):
+    for mf in (1, 3, 2):
         for a, b in zip(outs[mf], outs[0]):
             np.testing.assert_array_equal(a, b)
     if n <= 8:
