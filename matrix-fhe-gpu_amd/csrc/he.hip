@@ -158,6 +158,236 @@ __global__ __launch_bounds__(256) void enc_combine_kernel(const uint64_t* __rest
     }
 }
 
+// ---------------- fused X-axis ring product (n = 4..64) ----------------
+// t = INTT(NTT(a) (.) s) for one length-n row, phantom convention (the ph tables of mfhe_ntt_fwd/_inv, so
+// s = mfhe_ntt_fwd(secret) is in the matching order): the reference's xy_ntt_forward_phantom ->
+// pointwise_mul_s_kernel -> xy_ntt_backward_phantom (HE.cu:1500-1530, 1575-1590) without the three HBM
+// round trips.  T = n/4 lanes per row, lane j holds coefficients 4j..4j+3; butterflies at distance
+// t >= 4 pair lane j with lane j ^ (t/4), each lane of the pair computing two of the four butterflies;
+// t = 1, 2 stay in the lane.
+// FP64 exact modmul (ntt_arith.hpp); bounds: |mulmod| <= 1.5 q, forward values are re-centred every two
+// stages (|v| <= 2 q into a mulmod), inverse X every stage (|u - v| <= 3 q), q < 2^50.
+template <int LOGN>
+__device__ __forceinline__ void ring_mul_row(double (&x)[4], const double (&sv)[4], int j, const ArithF64& ar,
+                                             const double* __restrict__ tw, const double* __restrict__ itw,
+                                             double ninv) {
+#pragma unroll
+    for (int st = 0; st < LOGN; ++st) {   // forward CT: m = 2^st, t = n / 2m, W = tw[m + k / 2t]
+        const int m = 1 << st, lt = LOGN - 1 - st, t = 1 << lt;
+        if (t >= 4) {
+            // lanes j (lower) and j ^ d (upper) pair slot by slot; the lower lane computes slots 0, 1 and the
+            // upper slots 2, 3 (two shuffles in, two out, two modmuls per lane)
+            const int d = t >> 2;
+            const bool up = j & d;
+#pragma unroll
+            for (int k = 0; k < 2; ++k) {
+                const double recv = __shfl_xor(up ? x[k] : x[k + 2], d);
+                const double u = up ? recv : x[k], v = up ? x[k + 2] : recv;
+                const double mv = ar.mulmod(v, tw[m + ((4 * j + (up ? k + 2 : k)) >> (lt + 1))]);
+                const double X = u + mv, Y = u - mv;
+                const double back = __shfl_xor(up ? X : Y, d);
+                x[k] = up ? back : X;
+                x[k + 2] = up ? Y : back;
+            }
+        } else if (t == 2) {
+            const double w = tw[m + j];
+#pragma unroll
+            for (int a = 0; a < 2; ++a) {
+                const double mv = ar.mulmod(x[a + 2], w);
+                x[a + 2] = x[a] - mv;
+                x[a] += mv;
+            }
+        } else {
+#pragma unroll
+            for (int a = 0; a < 4; a += 2) {
+                const double mv = ar.mulmod(x[a + 1], tw[m + 2 * j + a / 2]);
+                x[a + 1] = x[a] - mv;
+                x[a] += mv;
+            }
+        }
+        if ((st & 1) || st == LOGN - 1)
+#pragma unroll
+            for (int s = 0; s < 4; ++s) x[s] = ar.reduce(x[s]);
+    }
+#pragma unroll
+    for (int s = 0; s < 4; ++s) x[s] = ar.mulmod(x[s], sv[s]);
+#pragma unroll
+    for (int st = LOGN - 1; st >= 0; --st) {   // inverse GS: X = u + v, Y = (u - v) W; m = 1 scales by n^-1
+        const int m = 1 << st, lt = LOGN - 1 - st, t = 1 << lt;
+        const bool last = st == 0;
+        auto xsum = [&](double u) { return last ? ar.mulmod(u, ninv) : ar.reduce(u); };
+        if (t >= 4) {
+            const int d = t >> 2;
+            const bool up = j & d;
+#pragma unroll
+            for (int k = 0; k < 2; ++k) {
+                const double recv = __shfl_xor(up ? x[k] : x[k + 2], d);
+                const double u = up ? recv : x[k], v = up ? x[k + 2] : recv;
+                const double X = xsum(u + v);
+                const double Y = ar.mulmod(u - v, itw[m + ((4 * j + (up ? k + 2 : k)) >> (lt + 1))]);
+                const double back = __shfl_xor(up ? X : Y, d);
+                x[k] = up ? back : X;
+                x[k + 2] = up ? Y : back;
+            }
+        } else if (t == 2) {
+            const double w = itw[m + j];
+#pragma unroll
+            for (int a = 0; a < 2; ++a) {
+                const double u = x[a], v = x[a + 2];
+                x[a] = xsum(u + v);
+                x[a + 2] = ar.mulmod(u - v, w);
+            }
+        } else {
+#pragma unroll
+            for (int a = 0; a < 4; a += 2) {
+                const double u = x[a], v = x[a + 1];
+                x[a] = xsum(u + v);
+                x[a + 1] = ar.mulmod(u - v, itw[m + 2 * j + a / 2]);
+            }
+        }
+    }
+}
+
+// 4 consecutive u64 (32-byte aligned) as two 16-byte accesses
+__device__ __forceinline__ void ld4(const uint64_t* p, uint64_t (&v)[4]) {
+    const ulonglong2 a = *(const ulonglong2*)p, b = *(const ulonglong2*)(p + 2);
+    v[0] = a.x; v[1] = a.y; v[2] = b.x; v[3] = b.y;
+}
+__device__ __forceinline__ void st4(uint64_t* p, const uint64_t (&v)[4]) {
+    *(ulonglong2*)p = make_ulonglong2(v[0], v[1]);
+    *(ulonglong2*)(p + 2) = make_ulonglong2(v[2], v[3]);
+}
+
+__device__ __forceinline__ double centred_f(uint64_t v, double q) {
+    const double d = ArithF64::from_u64(v);
+    return d > 0.5 * q ? d - q : d;
+}
+
+struct RingArgs {
+    const LimbConst* lf;     // [L]
+    const double* tw;        // ph_f tables [L][n]
+    const double* itw;
+    const double* ninv;      // [L]
+    const uint64_t* sk;      // [w][L][n], NTT form
+    int L;
+    uint64_t rows;           // 512 n L
+};
+
+// encrypt, fused: t = a * s over X (ring_mul_row), then encrypt_pair's combine (HE.cu:1530-1552):
+// ct_k.b = m_k - t + e, ct_k.a = a, written matrix-major; a, e poly-major.  One thread: 4 coefficients
+// of matrix row R = (w L + l) n + y.
+template <int LOGN>
+__global__ __launch_bounds__(256) void enc_ring_kernel(RingArgs ra, const uint64_t* __restrict__ aev,
+                                                       const uint64_t* __restrict__ e, const uint64_t* __restrict__ m_re,
+                                                       const uint64_t* __restrict__ m_im, uint64_t* __restrict__ ct_re,
+                                                       uint64_t* __restrict__ ct_im) {
+    constexpr int N = 1 << LOGN, T = N / 4;
+    const uint64_t g = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x;
+    const int j = (int)(g % T);
+    const uint64_t R = g / T;
+    const bool live = R < ra.rows;                     // dead lanes still take part in the shuffles
+    const uint64_t Rc = live ? R : 0;
+    const uint64_t y = Rc % N, wl = Rc / N, l = wl % ra.L, w = wl / ra.L;
+    const uint64_t i0 = Rc * N + 4 * j;                                  // matrix-major
+    const uint64_t p0 = ((w * N + y) * ra.L + l) * N + 4 * j;            // poly-major
+    const LimbConst lc = ra.lf[l];
+    const ArithF64 ar(lc);
+    uint64_t av[4], sk[4];
+    ld4(aev + p0, av);
+    ld4(ra.sk + (w * ra.L + l) * N + 4 * j, sk);
+    double x[4], sv[4];
+#pragma unroll
+    for (int s = 0; s < 4; ++s) {
+        x[s] = ArithF64::from_u64(av[s]);
+        sv[s] = centred_f(sk[s], lc.qf);
+    }
+    ring_mul_row<LOGN>(x, sv, j, ar, ra.tw + l * N, ra.itw + l * N, ra.ninv[l]);
+    if (!live) return;
+    const uint64_t q = lc.q, total = ra.rows * N;
+    uint64_t ev[4], mv[4], b[4];
+    ld4(e + p0, ev);
+    auto bval = [&](uint64_t m, int s) {
+        const uint64_t tv = ar.canon(x[s]);
+        uint64_t d = m >= tv ? m - tv : m + q - tv;
+        d += ev[s];
+        return d >= q ? d - q : d;
+    };
+    ld4(m_re + i0, mv);
+#pragma unroll
+    for (int s = 0; s < 4; ++s) b[s] = bval(mv[s], s);
+    st4(ct_re + i0, b);
+    st4(ct_re + total + i0, av);
+    if (m_im) {
+        ld4(m_im + i0, mv);
+#pragma unroll
+        for (int s = 0; s < 4; ++s) b[s] = bval(mv[s], s);
+        st4(ct_im + i0, b);
+        st4(ct_im + total + i0, av);
+    }
+}
+
+// decrypt, fused: out = ct.b + INTT(NTT(ct.a) * s), ct matrix-major in, out poly-major (HE.cu:1553-1601:
+// matrix_to_poly, X-NTT, pointwise_mul_s, X-INTT, add_poly).
+template <int LOGN>
+__global__ __launch_bounds__(256) void dec_ring_kernel(RingArgs ra, const uint64_t* __restrict__ ct,
+                                                       uint64_t* __restrict__ out) {
+    constexpr int N = 1 << LOGN, T = N / 4;
+    const uint64_t g = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x;
+    const int j = (int)(g % T);
+    const uint64_t R = g / T;
+    const bool live = R < ra.rows;
+    const uint64_t Rc = live ? R : 0;
+    const uint64_t y = Rc % N, wl = Rc / N, l = wl % ra.L, w = wl / ra.L;
+    const uint64_t i0 = Rc * N + 4 * j, total = ra.rows * N;
+    const uint64_t p0 = ((w * N + y) * ra.L + l) * N + 4 * j;
+    const LimbConst lc = ra.lf[l];
+    const ArithF64 ar(lc);
+    uint64_t av[4], sk[4];
+    ld4(ct + total + i0, av);
+    ld4(ra.sk + (w * ra.L + l) * N + 4 * j, sk);
+    double x[4], sv[4];
+#pragma unroll
+    for (int s = 0; s < 4; ++s) {
+        x[s] = ArithF64::from_u64(av[s]);
+        sv[s] = centred_f(sk[s], lc.qf);
+    }
+    ring_mul_row<LOGN>(x, sv, j, ar, ra.tw + l * N, ra.itw + l * N, ra.ninv[l]);
+    if (!live) return;
+    uint64_t bv[4];
+    ld4(ct + i0, bv);
+#pragma unroll
+    for (int s = 0; s < 4; ++s) {
+        const uint64_t sum = bv[s] + ar.canon(x[s]);
+        bv[s] = sum >= lc.q ? sum - lc.q : sum;
+    }
+    st4(out + p0, bv);
+}
+
+static bool ring_fused_ok(const mfhe_ctx* c, int logn) {
+    return c->he_fused && c->f64_ok && c->ph_f.tw && logn >= 2 && logn <= 6;
+}
+
+static RingArgs ring_args(const mfhe_ctx* c, const uint64_t* sk, int L, uint64_t rows) {
+    RingArgs ra;
+    ra.lf = c->d_limbs;
+    ra.tw = c->ph_f.tw;
+    ra.itw = c->ph_f.itw;
+    ra.ninv = c->ph_f.ninv;
+    ra.sk = sk;
+    ra.L = L;
+    ra.rows = rows;
+    return ra;
+}
+
+#define MFHE_RING_DISPATCH(KERNEL, logn, grid, s, ...)                                       \
+    switch (logn) {                                                                           \
+        case 2: hipLaunchKernelGGL(KERNEL<2>, grid, dim3(256), 0, s, __VA_ARGS__); break;     \
+        case 3: hipLaunchKernelGGL(KERNEL<3>, grid, dim3(256), 0, s, __VA_ARGS__); break;     \
+        case 4: hipLaunchKernelGGL(KERNEL<4>, grid, dim3(256), 0, s, __VA_ARGS__); break;     \
+        case 5: hipLaunchKernelGGL(KERNEL<5>, grid, dim3(256), 0, s, __VA_ARGS__); break;     \
+        default: hipLaunchKernelGGL(KERNEL<6>, grid, dim3(256), 0, s, __VA_ARGS__); break;    \
+    }
+
 // decrypt epilogue, fused: out[p] = ct.b[i] + t[p] mod q (matrix_to_poly of b, then add_poly_kernel
 // HE.cu:549-560), over the poly-major index p.
 __global__ __launch_bounds__(256) void dec_combine_kernel(const uint64_t* __restrict__ ctb, const uint64_t* __restrict__ t,
@@ -494,12 +724,19 @@ static int encrypt_impl(mfhe_ctx* c, const uint64_t* m_re, const uint64_t* m_im,
     hipLaunchKernelGGL(uniform_kernel, g1(W), dim3(256), 0, s, ap, c->d_rns_mu, g.L, g.logn, W);
     MFHE_CHECK_LAUNCH("uniform_kernel");
     RC(wcrt_gemm(c, c->d_wV, ap, false, aev, WOut::Poly, false, s));
-    MFHE_HIP(hipMemcpyAsync(ant, aev, W * 8, hipMemcpyDeviceToDevice, s));
-    RC(mfhe_ntt_fwd(c, ant, 512 * g.n, 0, g.L, (mfhe_stream_t)s));
     // e: identical for re and im (seed depends only on the coefficient, HE.cu:605-608)
     hipLaunchKernelGGL(gaussian_kernel, g1(W / g.L), dim3(256), 0, s, ep, c->d_rns_mu, g.L, g.logn, W / g.L);
     MFHE_CHECK_LAUNCH("gaussian_kernel");
     RC(wcrt_gemm(c, c->d_wV, ep, false, eev, WOut::Poly, false, s));
+    if (ring_fused_ok(c, g.logn)) {
+        const uint64_t rows = W / g.n;
+        const RingArgs ra = ring_args(c, sk, g.L, rows);
+        MFHE_RING_DISPATCH(enc_ring_kernel, g.logn, g1(rows * (g.n / 4)), s, ra, aev, eev, m_re, m_im, ct_re, ct_im);
+        MFHE_CHECK_LAUNCH("enc_ring_kernel");
+        return MFHE_OK;
+    }
+    MFHE_HIP(hipMemcpyAsync(ant, aev, W * 8, hipMemcpyDeviceToDevice, s));
+    RC(mfhe_ntt_fwd(c, ant, 512 * g.n, 0, g.L, (mfhe_stream_t)s));
     // t = INTT(a_ntt * s)  (reuse ep as t)
     uint64_t* t = ep;
     if (W >= (1ull << 32)) return set_error(MFHE_EUNSUPPORTED, "ciphertext of 2^32 words or more");
@@ -516,6 +753,13 @@ static int encrypt_impl(mfhe_ctx* c, const uint64_t* m_re, const uint64_t* m_im,
 static int decrypt_impl(mfhe_ctx* c, const uint64_t* ct, const uint64_t* sk, uint64_t* out, hipStream_t s, Bump* pb) {
     const Geo2 g = geo(c);
     const uint64_t W = g.words;
+    if (ring_fused_ok(c, g.logn)) {
+        const uint64_t rows = W / g.n;
+        const RingArgs ra = ring_args(c, sk, g.L, rows);
+        MFHE_RING_DISPATCH(dec_ring_kernel, g.logn, g1(rows * (g.n / 4)), s, ra, ct, out);
+        MFHE_CHECK_LAUNCH("dec_ring_kernel");
+        return MFHE_OK;
+    }
     uint64_t* ap = pb->get<uint64_t>(W);
     uint64_t* t = pb->get<uint64_t>(W);
     RC(layout(c, ct + W, ap, true, s));

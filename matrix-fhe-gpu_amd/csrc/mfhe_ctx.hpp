@@ -87,6 +87,7 @@ struct mfhe_ctx {
     double* d_wfold = nullptr;   // [L][16] factored forward fold constants (gemm.hip mfma_digitize_fold_kernel)
     int wcrt_mfma = 1;           // MFHE_OPT_WCRT_MFMA
     int cgemm_mfma = 1;          // MFHE_OPT_CGEMM_MFMA
+    int he_fused = 1;            // MFHE_OPT_HE_FUSED
     void* gemm_ws = nullptr;     // B digit planes for the MFMA GEMM, grown on demand
     size_t gemm_ws_bytes = 0;
     size_t fused_bytes = 0;
