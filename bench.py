@@ -177,6 +177,50 @@ def pipeline_line(reps=10):
             "main_cu_check_1e-4": err < 1e-4}
 
 
+def trace_line(reps=10):
+    """Batched trace GEMM (batched_trace.cu:37-197) at the reference geometry: 512 matrices x L = 11 x
+    n = 64: map B -> B', C = n A B'^T (complex mod q), rescale.  FP64-VALU bound: 4 exact modmuls per complex
+    MAC, 512 * 11 * 64^3 complex MACs per call."""
+    import numpy as np
+    import torch
+    import mfhe
+    n, L, batch = 64, 11, 512
+    ctx = mfhe.Context(mfhe.RNS_MODULI, 1, mfhe.CONV_PHANTOM)
+    q = np.array(mfhe.RNS_MODULI, np.uint64)[None, :, None]
+    rng = np.random.default_rng(5)
+    planes = [mfhe.to_device_u64((rng.integers(0, 2 ** 63, (batch, L, n * n), dtype=np.uint64) % q).ravel())
+              for _ in range(4)]
+    bp = [torch.empty_like(planes[0]) for _ in range(2)]
+    c = [torch.empty_like(planes[0]) for _ in range(2)]
+    inv = [pow(2 ** 35, -1, int(m)) for m in mfhe.RNS_MODULI[:3]] + [0] * (L - 3)
+
+    def gemm():
+        ctx.trace_gemm(planes[0], planes[1], bp[0], bp[1], c[0], c[1], n, L, batch)
+
+    def full():
+        ctx.trace_map_bprime(planes[2], planes[3], bp[0], bp[1], n, L, batch)
+        gemm()
+        ctx.trace_rescale(c[0], c[1], n, L, batch, inv)
+    full()
+    torch.cuda.synchronize()
+    e = [torch.cuda.Event(enable_timing=True) for _ in range(4)]
+    e[0].record()
+    for _ in range(reps):
+        gemm()
+    e[1].record()
+    for _ in range(reps):
+        full()
+    e[2].record()
+    torch.cuda.synchronize()
+    g_ms, f_ms = e[0].elapsed_time(e[1]) / reps, e[1].elapsed_time(e[2]) / reps
+    macs = batch * L * n ** 3
+    ctx.close()
+    return {"workload": "batched trace GEMM, 512 matrices x L=11 x n=64 complex mod q (reference geometry)",
+            "gemm_ms": round(g_ms, 3), "map_gemm_rescale_ms": round(f_ms, 3),
+            "complex_modmac_per_s": round(macs / (g_ms * 1e-3)),
+            "fp64_valu_tflops_est": round(macs * 4 * 6 / (g_ms * 1e-3) / 1e12, 1)}
+
+
 def cpu_baseline(log_n, moduli, seconds):
     """Reference CPU path restated (oracle, Harvey/Shoup phantom NTT, OpenMP over polys)."""
     import numpy as np
@@ -380,6 +424,7 @@ def main():
         if world == 1 and not args.no_pipeline and args.only == "all":
             out["reference_geometry_pipeline"] = pipeline_line()
             out["other_ntt_configs"] = other_configs_line()
+            out["trace_gemm_reference_geometry"] = trace_line()
         if world == 1 and not args.no_cpu_baseline and args.only == "all":
             try:
                 out["cpu_baseline"] = cpu_baseline(log_n, moduli, args.cpu_seconds)

@@ -151,6 +151,25 @@ class BatchedEncoder {
     int n_, n2_;
 };
 
+// ---- trace GEMM (reference include/core/trace.cuh, include/core/batched_trace.cuh) ----
+// Planes [batch][limbs][n][n]; moduli RNS_MODULI.  As in the reference, trace_gemm_batched /
+// trace_gemm_ABpT_rns run over all RNS_NUM_LIMBS limbs whatever rns_limbs says (batched_trace.cu:113-116,
+// trace.cu:90), map_B_to_Bprime_Xinv_twist and rescale_by_delta_rns likewise (trace.cu:45,137), and the
+// rescales multiply limbs >= 3 by 0 (batched_trace.cu:179, trace.cu:151-154).
+void map_B_to_Bprime_Xinv_twist(const uint64_t* B_real, const uint64_t* B_imag, uint64_t* Bp_real,
+                                uint64_t* Bp_imag, int n, int rns_limbs);
+void trace_gemm_ABpT_rns(const uint64_t* A_real, const uint64_t* A_imag, const uint64_t* Bp_real,
+                         const uint64_t* Bp_imag, uint64_t* C_real, uint64_t* C_imag, int n, int rns_limbs);
+void rescale_by_delta_rns(uint64_t* C_real, uint64_t* C_imag, int n, int rns_limbs, uint64_t inv0, uint64_t inv1,
+                          uint64_t inv2);
+void map_B_to_Bprime_batched(const uint64_t* B_real, const uint64_t* B_imag, uint64_t* Bp_real, uint64_t* Bp_imag,
+                             int n, int rns_limbs, int batch_size);
+void trace_gemm_batched(const uint64_t* A_real, const uint64_t* A_imag, const uint64_t* Bp_real,
+                        const uint64_t* Bp_imag, uint64_t* C_real, uint64_t* C_imag, int n, int rns_limbs,
+                        int batch_size);
+void rescale_by_delta_batched(uint64_t* C_real, uint64_t* C_imag, int n, int rns_limbs, int batch_size,
+                              uint64_t inv0, uint64_t inv1, uint64_t inv2);
+
 // The C-ABI context (include/mfhe.h) behind this API for a given (n, limbs): moduli RNS_MODULI[0..limbs),
 // delta = SCALING_FACTOR, phantom + GL (+ W-CRT when with_wcrt) tables.  Built once, cached.
 struct mfhe_ctx* backend_context(int n, int limbs, bool with_wcrt = false);

@@ -126,6 +126,10 @@ struct mfhe_ctx {
     double2* d_wdVinv = nullptr;   // [512][512]     its inverse (complex Gauss-Jordan)
     double2 *d_encV = nullptr, *d_encVT = nullptr, *d_encVi = nullptr, *d_encViT = nullptr;  // [n][n]
 
+    // trace GEMM (trace.hip): n mod q_l, centred, for the FP64 epilogue; built on first use for trace_n
+    double* d_trace_nmod = nullptr;   // [L]
+    int trace_n = 0;
+
     // pipeline workspace (allocated on first use / mfhe_ctx_reserve_workspace)
     void* ws = nullptr;
     size_t ws_bytes = 0;

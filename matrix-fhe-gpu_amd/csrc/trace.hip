@@ -1,0 +1,279 @@
+// trace.hip -- batched trace GEMM: the homomorphic matrix-product stage of the scheme.
+//
+// Reference: src/core/batched_trace.cu:37-197 (map_Bprime_batched_kernel, trace_gemm_batched_kernel,
+// rescale_by_delta_batched_kernel) and src/core/trace.cu:30-161 (the single-matrix versions).
+// Planes are [batch][nlimbs][n][n] u64, one array for the real and one for the imaginary part.
+//
+// The reference does four `unsigned __int128 %` (a software division) per complex MAC, one thread per
+// output.  Here a 256-thread workgroup computes a 64 x 64 output tile of one (batch, limb): 16-deep
+// k-panels of A and B' go global -> LDS once (centred, as exact doubles), every thread holds a 4 x 4
+// complex register tile, and each product is the FP64 error-free modmul of the NTT (ntt_arith.hpp).
+// The accumulators are exact integers in doubles, re-reduced every KR k-steps so they stay < 2^53;
+// the epilogue multiplies by n and canonicalises.  Same value mod q as the reference, so the canonical
+// output is bit-identical.  Moduli >= 2^50 or n not a multiple of 64 take a u128 kernel (one output per
+// thread, the reference's order of operations with a Barrett reduction in place of %).
+#include <hip/hip_runtime.h>
+
+#include "mfhe_ctx.hpp"
+
+namespace mfhe {
+
+namespace {
+
+constexpr int TR_TILE = 64;   // output tile edge
+constexpr int TR_KP = 16;     // k-panel depth staged in LDS
+constexpr int TR_LDS = 68;    // padded row stride (doubles): 2-way conflicts on the transposing store
+
+// (hi:lo) mod q: fold hi with r64 = 2^64 mod q, then Barrett with mu = floor(2^64 / q)
+__device__ __forceinline__ uint64_t tr_mod128(unsigned __int128 v, uint64_t q, uint64_t mu, uint64_t r64) {
+    uint64_t hi = (uint64_t)(v >> 64), lo = (uint64_t)v;
+    while (hi) {
+        const unsigned __int128 t = (unsigned __int128)hi * r64 + lo;
+        hi = (uint64_t)(t >> 64);
+        lo = (uint64_t)t;
+    }
+    uint64_t r = lo - __umul64hi(lo, mu) * q;
+    r = r >= q ? r - q : r;
+    return r >= q ? r - q : r;
+}
+
+// map_Bprime_batched_kernel (batched_trace.cu:37-79): conj(B), row j -> (n - j) mod n, rows j != 0 times -i.
+__global__ void trace_map_kernel(const uint64_t* __restrict__ br, const uint64_t* __restrict__ bi,
+                                 uint64_t* __restrict__ opr, uint64_t* __restrict__ opi, const uint64_t* qmu,
+                                 int log_n, int L, uint64_t total) {
+    const uint64_t idx = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x;
+    if (idx >= total) return;
+    const uint64_t n = 1ull << log_n, n2 = n << log_n;
+    const uint64_t mat = idx >> (2 * log_n), pos = idx & (n2 - 1);
+    const uint64_t j = pos >> log_n, k = pos & (n - 1);
+    const uint64_t q = qmu[2 * (mat % (uint64_t)L)];
+    const uint64_t a = br[idx], b = bi[idx];
+    const uint64_t na = a ? q - a : 0, nb = b ? q - b : 0;
+    const uint64_t dst = mat * n2 + (((n - j) & (n - 1)) << log_n) + k;
+    opr[dst] = j == 0 ? a : nb;
+    opi[dst] = j == 0 ? nb : na;
+}
+
+// trace_gemm_batched_kernel (batched_trace.cu:99-146), FP64 tile kernel (every q < 2^50, n % 64 == 0).
+// KR: k-steps between accumulator reductions; each step adds two products of magnitude < 1.5 q, so
+// |acc| < (0.5 + 3 KR) q must stay below 2^53 (host picks KR = 16 for q < 2^47.4, else 2).
+template <int KR>
+__global__ __launch_bounds__(256) void trace_gemm_f64_kernel(
+    const uint64_t* __restrict__ Ar, const uint64_t* __restrict__ Ai, const uint64_t* __restrict__ Br,
+    const uint64_t* __restrict__ Bi, uint64_t* __restrict__ Cr, uint64_t* __restrict__ Ci,
+    const LimbConst* __restrict__ lf, const double* __restrict__ nmod, int log_n, int L) {
+    __shared__ double sA[2][TR_KP][TR_LDS];
+    __shared__ double sB[2][TR_KP][TR_LDS];
+    const int n = 1 << log_n, tdim = n / TR_TILE, tiles = tdim * tdim;
+    const uint64_t mat = blockIdx.x / tiles;
+    const int tile = blockIdx.x % tiles, tm = tile / tdim, tn = tile % tdim;
+    const int l = (int)(mat % (uint64_t)L);
+    const ArithF64 ar(lf[l]);
+    const double q = ar.q, qh = 0.5 * q;
+    const uint64_t base = mat << (2 * log_n);
+    const uint64_t* a_re = Ar + base + (uint64_t)(tm * TR_TILE) * n;
+    const uint64_t* a_im = Ai + base + (uint64_t)(tm * TR_TILE) * n;
+    const uint64_t* b_re = Br + base + (uint64_t)(tn * TR_TILE) * n;
+    const uint64_t* b_im = Bi + base + (uint64_t)(tn * TR_TILE) * n;
+    const int tid = threadIdx.x, tx = tid & 15, ty = tid >> 4;
+
+    double accr[4][4], acci[4][4];
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+#pragma unroll
+        for (int j = 0; j < 4; ++j) accr[i][j] = acci[i][j] = 0.0;
+
+    for (int k0 = 0; k0 < n; k0 += TR_KP) {
+        // stage: 64 rows x 16 k of each plane; a thread loads 4 elements per plane (row-contiguous 128 B runs)
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+            const int idx = tid + 256 * e, r = idx >> 4, kk = idx & 15;
+            const uint64_t g = (uint64_t)r * n + k0 + kk;
+            const double v0 = ArithF64::from_u64(a_re[g]), v1 = ArithF64::from_u64(a_im[g]);
+            const double v2 = ArithF64::from_u64(b_re[g]), v3 = ArithF64::from_u64(b_im[g]);
+            sA[0][kk][r] = v0 > qh ? v0 - q : v0;
+            sA[1][kk][r] = v1 > qh ? v1 - q : v1;
+            sB[0][kk][r] = v2 > qh ? v2 - q : v2;
+            sB[1][kk][r] = v3 > qh ? v3 - q : v3;
+        }
+        __syncthreads();
+#pragma unroll 2
+        for (int kk = 0; kk < TR_KP; ++kk) {
+            double xr[4], xi[4], yr[4], yi[4];
+#pragma unroll
+            for (int i = 0; i < 4; ++i) {
+                xr[i] = sA[0][kk][ty + 16 * i];
+                xi[i] = sA[1][kk][ty + 16 * i];
+                yr[i] = sB[0][kk][tx + 16 * i];
+                yi[i] = sB[1][kk][tx + 16 * i];
+            }
+#pragma unroll
+            for (int i = 0; i < 4; ++i)
+#pragma unroll
+                for (int j = 0; j < 4; ++j) {
+                    accr[i][j] += ar.mulmod(xr[i], yr[j]) - ar.mulmod(xi[i], yi[j]);
+                    acci[i][j] += ar.mulmod(xr[i], yi[j]) + ar.mulmod(xi[i], yr[j]);
+                }
+            if ((kk + 1) % KR == 0) {
+#pragma unroll
+                for (int i = 0; i < 4; ++i)
+#pragma unroll
+                    for (int j = 0; j < 4; ++j) {
+                        accr[i][j] = ar.reduce(accr[i][j]);
+                        acci[i][j] = ar.reduce(acci[i][j]);
+                    }
+            }
+        }
+        __syncthreads();
+    }
+    const double nm = nmod[l];   // n mod q, centred
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+            const uint64_t o = base + (uint64_t)(tm * TR_TILE + ty + 16 * i) * n + tn * TR_TILE + tx + 16 * j;
+            Cr[o] = ar.canon(ar.mulmod(ar.reduce(accr[i][j]), nm));
+            Ci[o] = ar.canon(ar.mulmod(ar.reduce(acci[i][j]), nm));
+        }
+}
+
+// Any q < 2^62, any n: one output per thread, the reference's sequence (batched_trace.cu:124-144).
+__global__ void trace_gemm_u128_kernel(const uint64_t* __restrict__ Ar, const uint64_t* __restrict__ Ai,
+                                       const uint64_t* __restrict__ Br, const uint64_t* __restrict__ Bi,
+                                       uint64_t* __restrict__ Cr, uint64_t* __restrict__ Ci, const uint64_t* qmu,
+                                       const uint64_t* r64, int log_n, int L, uint64_t total) {
+    const uint64_t idx = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x;
+    if (idx >= total) return;
+    const int n = 1 << log_n;
+    const uint64_t mat = idx >> (2 * log_n), pos = idx & ((1ull << (2 * log_n)) - 1);
+    const uint64_t row = pos >> log_n, col = pos & (n - 1), base = mat << (2 * log_n);
+    const int l = (int)(mat % (uint64_t)L);
+    const uint64_t q = qmu[2 * l], mu = qmu[2 * l + 1], rr = r64[l];
+    using u128 = unsigned __int128;
+    uint64_t acc_r = 0, acc_i = 0;
+    for (int t = 0; t < n; ++t) {
+        const uint64_t ar = Ar[base + row * n + t], ai = Ai[base + row * n + t];
+        const uint64_t br = Br[base + col * n + t], bi = Bi[base + col * n + t];
+        const uint64_t rrp = tr_mod128((u128)ar * br, q, mu, rr), iip = tr_mod128((u128)ai * bi, q, mu, rr);
+        const uint64_t rip = tr_mod128((u128)ar * bi, q, mu, rr), irp = tr_mod128((u128)ai * br, q, mu, rr);
+        const uint64_t pr = rrp >= iip ? rrp - iip : q - (iip - rrp);
+        uint64_t pi = rip + irp;
+        pi = pi >= q ? pi - q : pi;
+        uint64_t s = acc_r + pr;
+        acc_r = s >= q ? s - q : s;
+        s = acc_i + pi;
+        acc_i = s >= q ? s - q : s;
+    }
+    const uint64_t nm = (uint64_t)n % q;
+    Cr[idx] = tr_mod128((u128)acc_r * nm, q, mu, rr);
+    Ci[idx] = tr_mod128((u128)acc_i * nm, q, mu, rr);
+}
+
+struct RescaleArgs {
+    uint64_t w[64];    // inv[l] mod q_l
+    uint64_t ws[64];   // floor(w 2^64 / q_l) (Shoup)
+};
+
+// rescale_by_delta_batched_kernel (batched_trace.cu:163-183): C *= inv[l] mod q_l
+__global__ void trace_rescale_kernel(uint64_t* Cr, uint64_t* Ci, const uint64_t* qmu, RescaleArgs a, int log_n2,
+                                     int L, uint64_t total) {
+    const uint64_t idx = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x;
+    if (idx >= total) return;
+    const int l = (int)((idx >> log_n2) % (uint64_t)L);
+    const uint64_t q = qmu[2 * l], w = a.w[l], ws = a.ws[l];
+    uint64_t x = Cr[idx], r = x * w - __umul64hi(x, ws) * q;
+    Cr[idx] = r >= q ? r - q : r;
+    x = Ci[idx];
+    r = x * w - __umul64hi(x, ws) * q;
+    Ci[idx] = r >= q ? r - q : r;
+}
+
+inline dim3 g1(uint64_t total, uint32_t th = 256) { return dim3((uint32_t)((total + th - 1) / th)); }
+
+int trace_check(const mfhe_ctx* c, int n, int nlimbs, size_t batch, const char* what) {
+    if (!c) return set_error(MFHE_EINVAL, std::string(what) + ": null ctx");
+    if (n < 2 || n > 1024 || (n & (n - 1)))
+        return set_error(MFHE_EINVAL, std::string(what) + ": n must be a power of two in [2, 1024]");
+    if (nlimbs < 1 || nlimbs > c->L)
+        return set_error(MFHE_EINVAL, std::string(what) + ": nlimbs must be in [1, ctx limbs]");
+    if (batch == 0) return set_error(MFHE_EINVAL, std::string(what) + ": batch must be >= 1");
+    return MFHE_OK;
+}
+
+int ilog2(int n) { return 31 - __builtin_clz((unsigned)n); }
+
+}  // namespace
+}  // namespace mfhe
+
+using namespace mfhe;
+
+extern "C" int mfhe_trace_map_bprime(mfhe_ctx* c, const uint64_t* br, const uint64_t* bi, uint64_t* opr,
+                                     uint64_t* opi, int n, int nlimbs, size_t batch, mfhe_stream_t s) {
+    if (int rc = trace_check(c, n, nlimbs, batch, "mfhe_trace_map_bprime")) return rc;
+    if (!br || !bi || !opr || !opi) return set_error(MFHE_EINVAL, "mfhe_trace_map_bprime: null pointer");
+    if (br == opr || bi == opi || br == opi || bi == opr)
+        return set_error(MFHE_EINVAL, "mfhe_trace_map_bprime: output must not alias input");
+    const uint64_t total = (uint64_t)batch * nlimbs * n * n;
+    hipLaunchKernelGGL(trace_map_kernel, g1(total), dim3(256), 0, (hipStream_t)s, br, bi, opr, opi, c->d_rns_mu,
+                       ilog2(n), nlimbs, total);
+    MFHE_CHECK_LAUNCH("trace_map_kernel");
+    return MFHE_OK;
+}
+
+extern "C" int mfhe_trace_gemm(mfhe_ctx* c, const uint64_t* ar, const uint64_t* ai, const uint64_t* bpr,
+                               const uint64_t* bpi, uint64_t* cr, uint64_t* ci, int n, int nlimbs, size_t batch,
+                               mfhe_stream_t s) {
+    if (int rc = trace_check(c, n, nlimbs, batch, "mfhe_trace_gemm")) return rc;
+    if (!ar || !ai || !bpr || !bpi || !cr || !ci) return set_error(MFHE_EINVAL, "mfhe_trace_gemm: null pointer");
+    const uint64_t total = (uint64_t)batch * nlimbs * n * n;
+    const int log_n = ilog2(n);
+    if (c->f64_ok && n % TR_TILE == 0) {
+        if (!c->d_trace_nmod || c->trace_n != n) {   // n mod q_l, centred, per limb (rebuilt when n changes)
+            if (!c->d_trace_nmod) {
+                MFHE_HIP(hipMalloc(&c->d_trace_nmod, sizeof(double) * c->L));
+                c->allocs.push_back(c->d_trace_nmod);
+            }
+            std::vector<double> nm(c->L);
+            for (int l = 0; l < c->L; ++l) {
+                const uint64_t q = c->moduli[l], v = (uint64_t)n % q;
+                nm[l] = v > q / 2 ? (double)v - (double)q : (double)v;
+            }
+            MFHE_HIP(hipMemcpy(c->d_trace_nmod, nm.data(), sizeof(double) * c->L, hipMemcpyHostToDevice));
+            c->trace_n = n;
+        }
+        uint64_t qmax = 0;
+        for (int l = 0; l < nlimbs; ++l) qmax = c->moduli[l] > qmax ? c->moduli[l] : qmax;
+        const uint64_t blocks = (uint64_t)batch * nlimbs * (n / TR_TILE) * (n / TR_TILE);
+        if (blocks > 0x7fffffffull) return set_error(MFHE_EINVAL, "mfhe_trace_gemm: batch too large");
+        if ((double)qmax * 48.5 < 9007199254740992.0)   // (0.5 + 3 * 16) q < 2^53
+            hipLaunchKernelGGL(trace_gemm_f64_kernel<16>, dim3((uint32_t)blocks), dim3(256), 0, (hipStream_t)s, ar,
+                               ai, bpr, bpi, cr, ci, c->d_limbs, c->d_trace_nmod, log_n, nlimbs);
+        else
+            hipLaunchKernelGGL(trace_gemm_f64_kernel<2>, dim3((uint32_t)blocks), dim3(256), 0, (hipStream_t)s, ar,
+                               ai, bpr, bpi, cr, ci, c->d_limbs, c->d_trace_nmod, log_n, nlimbs);
+        MFHE_CHECK_LAUNCH("trace_gemm_f64_kernel");
+        return MFHE_OK;
+    }
+    hipLaunchKernelGGL(trace_gemm_u128_kernel, g1(total), dim3(256), 0, (hipStream_t)s, ar, ai, bpr, bpi, cr, ci,
+                       c->d_rns_mu, c->d_r64, log_n, nlimbs, total);
+    MFHE_CHECK_LAUNCH("trace_gemm_u128_kernel");
+    return MFHE_OK;
+}
+
+extern "C" int mfhe_trace_rescale(mfhe_ctx* c, uint64_t* cr, uint64_t* ci, int n, int nlimbs, size_t batch,
+                                  const uint64_t* inv, mfhe_stream_t s) {
+    if (int rc = trace_check(c, n, nlimbs, batch, "mfhe_trace_rescale")) return rc;
+    if (!cr || !ci || !inv) return set_error(MFHE_EINVAL, "mfhe_trace_rescale: null pointer");
+    if (nlimbs > 64) return set_error(MFHE_EINVAL, "mfhe_trace_rescale: at most 64 limbs");
+    RescaleArgs a{};
+    for (int l = 0; l < nlimbs; ++l) {
+        const uint64_t q = c->moduli[l];
+        a.w[l] = inv[l] % q;
+        a.ws[l] = (uint64_t)(((unsigned __int128)a.w[l] << 64) / q);
+    }
+    const uint64_t total = (uint64_t)batch * nlimbs * n * n;
+    hipLaunchKernelGGL(trace_rescale_kernel, g1(total), dim3(256), 0, (hipStream_t)s, cr, ci, c->d_rns_mu, a,
+                       2 * ilog2(n), nlimbs, total);
+    MFHE_CHECK_LAUNCH("trace_rescale_kernel");
+    return MFHE_OK;
+}

@@ -103,6 +103,9 @@ _sig("mfhe_wdft_fwd_pair_i64", [_vp] * 6)
 _sig("mfhe_wdft_inv_pair", [_vp] * 6)
 _sig("mfhe_ct_add", [_vp] * 5)
 _sig("mfhe_ct_mul_tensor", [_vp] * 7)
+_sig("mfhe_trace_map_bprime", [_vp] * 5 + [ctypes.c_int, ctypes.c_int, _sz, _vp])
+_sig("mfhe_trace_gemm", [_vp] * 7 + [ctypes.c_int, ctypes.c_int, _sz, _vp])
+_sig("mfhe_trace_rescale", [_vp] * 3 + [ctypes.c_int, ctypes.c_int, _sz, _u64p, _vp])
 _sig("mfhe_ctx_reserve_workspace", [_vp])
 _sig("mfhe_encode", [_vp, _vp, _vp, _vp, _vp])
 _sig("mfhe_decode", [_vp, _vp, _vp, _vp, _vp])
@@ -287,6 +290,17 @@ class Context:
         self._call("mfhe_ct_add", _ptr(ct1), _ptr(ct2), _ptr(res), stream=stream); return res
     def ct_mul_tensor(self, ct1, ct2, d0, d1, d2, stream=None):
         self._call("mfhe_ct_mul_tensor", _ptr(ct1), _ptr(ct2), _ptr(d0), _ptr(d1), _ptr(d2), stream=stream)
+    # ---- trace GEMM, planes [batch][nlimbs][n][n] (batched_trace.cu) ----
+    def trace_map_bprime(self, b_re, b_im, bp_re, bp_im, n, nlimbs, batch, stream=None):
+        check(lib.mfhe_trace_map_bprime(self._h, _ptr(b_re), _ptr(b_im), _ptr(bp_re), _ptr(bp_im), n, nlimbs, batch,
+                                        _stream_ptr(stream)), "trace_map_bprime")
+    def trace_gemm(self, a_re, a_im, bp_re, bp_im, c_re, c_im, n, nlimbs, batch, stream=None):
+        check(lib.mfhe_trace_gemm(self._h, _ptr(a_re), _ptr(a_im), _ptr(bp_re), _ptr(bp_im), _ptr(c_re), _ptr(c_im),
+                                  n, nlimbs, batch, _stream_ptr(stream)), "trace_gemm")
+    def trace_rescale(self, c_re, c_im, n, nlimbs, batch, inv, stream=None):
+        arr = (ctypes.c_uint64 * nlimbs)(*[int(v) for v in inv[:nlimbs]])
+        check(lib.mfhe_trace_rescale(self._h, _ptr(c_re), _ptr(c_im), n, nlimbs, batch, arr, _stream_ptr(stream)),
+              "trace_rescale")
     def xy_dft(self, src, dst, lanes, stream=None):
         check(lib.mfhe_xy_dft(self._h, _ptr(src), _ptr(dst), lanes, _stream_ptr(stream)), "xy_dft"); return dst
     def xy_idft(self, src, dst, lanes, stream=None):

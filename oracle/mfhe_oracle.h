@@ -154,6 +154,15 @@ int     orc_he_words(orc_he* h);
 const uint64_t* orc_he_V(orc_he* h);
 const uint64_t* orc_he_VinvT(orc_he* h);
 
+/* ---------------- trace GEMM (batched_trace.cu:37-197, trace.cu:30-161) ----------------- */
+/* Layout [batch][L][n][n] per real / imaginary plane; limb l uses moduli[l]. */
+void orc_trace_map_bprime(const uint64_t* Br, const uint64_t* Bi, uint64_t* Bpr, uint64_t* Bpi, int n, int L,
+                          size_t batch, const uint64_t* moduli);
+void orc_trace_gemm(const uint64_t* Ar, const uint64_t* Ai, const uint64_t* Br, const uint64_t* Bi, uint64_t* Cr,
+                    uint64_t* Ci, int n, int L, size_t batch, const uint64_t* moduli);
+void orc_trace_rescale(uint64_t* Cr, uint64_t* Ci, int n, int L, size_t batch, const uint64_t* moduli,
+                       const uint64_t* inv);
+
 #ifdef __cplusplus
 }
 #endif

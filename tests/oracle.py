@@ -85,6 +85,9 @@ _s("orc_he_decode_stages", [vp] + [vp] * 13)
 _s("orc_he_words", [vp], ci)
 _s("orc_he_V", [vp], vp)
 _s("orc_he_VinvT", [vp], vp)
+_s("orc_trace_map_bprime", [vp, vp, vp, vp, ci, ci, sz, vp])
+_s("orc_trace_gemm", [vp, vp, vp, vp, vp, vp, ci, ci, sz, vp])
+_s("orc_trace_rescale", [vp, vp, ci, ci, sz, vp, vp])
 
 
 def P(a: np.ndarray):
@@ -189,6 +192,27 @@ def wcrt_tables(q: int, gauss: bool = False):
     rc = L.orc_wcrt_tables(q, P(V), P(Vi), int(gauss))
     assert rc == 0
     return V, Vi
+
+
+# ---- trace GEMM, [batch][L][n][n] planes (batched_trace.cu) ----
+def trace_map_bprime(br, bi, n, L_, batch, moduli):
+    br, bi = U64(br), U64(bi)
+    opr, opi = np.zeros_like(br), np.zeros_like(bi)
+    L.orc_trace_map_bprime(P(br), P(bi), P(opr), P(opi), n, L_, batch, P(U64(moduli)))
+    return opr, opi
+
+
+def trace_gemm(ar, ai, br, bi, n, L_, batch, moduli):
+    ar, ai, br, bi = U64(ar), U64(ai), U64(br), U64(bi)
+    cr, ci_ = np.zeros_like(ar), np.zeros_like(ai)
+    L.orc_trace_gemm(P(ar), P(ai), P(br), P(bi), P(cr), P(ci_), n, L_, batch, P(U64(moduli)))
+    return cr, ci_
+
+
+def trace_rescale(cr, ci_, n, L_, batch, moduli, inv):
+    cr, ci_ = U64(cr).copy(), U64(ci_).copy()
+    L.orc_trace_rescale(P(cr), P(ci_), n, L_, batch, P(U64(moduli)), P(U64(inv)))
+    return cr, ci_
 
 
 class HE:

@@ -1,0 +1,113 @@
+"""Trace GEMM (src/core/batched_trace.cu:37-197, src/core/trace.cu:30-161): B -> B', C = n A B'^T and the
+rescale, [batch][L][n][n] planes.
+
+The reference has no test for this stage, so parity is anchored on the oracle restatement
+(orc_trace_*, the reference's exact add_mod / sub_mod / mul_mod_u128 sequence), itself checked here
+against an independent Python-integer computation of the same linear algebra.  Parity with reference
+outputs is unpinned (no reference run is possible here).  Integer work: bit-exact.
+"""
+import numpy as np
+import pytest
+
+RNS = [17592186435073, 17182765057, 17184541441, 17186120449, 17186515201, 17186909953,
+       17188883713, 17190462721, 17190857473, 17191844353, 17192831233]
+
+
+def _rand(rng, batch, L, n, moduli):
+    q = np.array(moduli[:L], np.uint64)[None, :, None]
+    return (rng.integers(0, 2 ** 63, (batch, L, n * n), dtype=np.uint64) % q).ravel()
+
+
+def _py_trace(ar, ai, br, bi, n, L, batch, moduli):
+    """Independent restatement with Python integers: map B -> B', then C = n A B'^T (complex mod q)."""
+    shp = (batch, L, n, n)
+    ar, ai, br, bi = (x.reshape(shp).astype(object) for x in (ar, ai, br, bi))
+    cr = np.zeros(shp, dtype=object)
+    ci = np.zeros(shp, dtype=object)
+    for b in range(batch):
+        for l in range(L):
+            q = int(moduli[l])
+            # B'(X) = conj(B)(X^-1) with X^n = i: row j -> -j, times -i for j != 0
+            pr = np.zeros((n, n), dtype=object)
+            pi = np.zeros((n, n), dtype=object)
+            for j in range(n):
+                re, im = br[b, l, j], (-bi[b, l, j]) % q
+                if j:
+                    re, im = im, (-br[b, l, j]) % q      # (-i)(re + i im) = im - i re
+                pr[(-j) % n], pi[(-j) % n] = re, im
+            A_r, A_i = ar[b, l], ai[b, l]
+            cr[b, l] = (n * (A_r.dot(pr.T) - A_i.dot(pi.T))) % q
+            ci[b, l] = (n * (A_r.dot(pi.T) + A_i.dot(pr.T))) % q
+    return cr.ravel().astype(np.uint64), ci.ravel().astype(np.uint64)
+
+
+def test_oracle_trace_matches_python_integers(orc):
+    rng = np.random.default_rng(7)
+    n, L, batch = 8, 3, 2
+    ar, ai, br, bi = (_rand(rng, batch, L, n, RNS) for _ in range(4))
+    bpr, bpi = orc.trace_map_bprime(br, bi, n, L, batch, RNS)
+    cr, ci = orc.trace_gemm(ar, ai, bpr, bpi, n, L, batch, RNS)
+    er, ei = _py_trace(ar, ai, br, bi, n, L, batch, RNS)
+    np.testing.assert_array_equal(cr, er)
+    np.testing.assert_array_equal(ci, ei)
+    # rescale: the reference's (inv0, inv1, inv2) call leaves limbs >= 3 multiplied by 0
+    inv = [orc.L.orc_invmod(2 ** 35 % q, q) for q in RNS[:L]]
+    sr, si = orc.trace_rescale(cr, ci, n, L, batch, RNS, inv)
+    for l in range(L):
+        q = RNS[l]
+        v = cr.reshape(batch, L, -1)[:, l].astype(object) * inv[l] % q
+        np.testing.assert_array_equal(sr.reshape(batch, L, -1)[:, l], v.astype(np.uint64))
+
+
+def _gpu_case(mfhe, orc, moduli, log_n_ctx, n, L, batch, seed):
+    import torch
+    ctx = mfhe.Context(moduli, log_n_ctx, mfhe.CONV_PHANTOM)
+    rng = np.random.default_rng(seed)
+    ar, ai, br, bi = (_rand(rng, batch, L, n, moduli) for _ in range(4))
+    d = [mfhe.to_device_u64(x) for x in (ar, ai, br, bi)]
+    bp = [torch.empty_like(d[0]), torch.empty_like(d[0])]
+    c = [torch.empty_like(d[0]), torch.empty_like(d[0])]
+    ctx.trace_map_bprime(d[2], d[3], bp[0], bp[1], n, L, batch)
+    ctx.trace_gemm(d[0], d[1], bp[0], bp[1], c[0], c[1], n, L, batch)
+    torch.cuda.synchronize()
+    obpr, obpi = orc.trace_map_bprime(br, bi, n, L, batch, moduli)
+    np.testing.assert_array_equal(mfhe.to_host_u64(bp[0]), obpr)
+    np.testing.assert_array_equal(mfhe.to_host_u64(bp[1]), obpi)
+    ocr, oci = orc.trace_gemm(ar, ai, obpr, obpi, n, L, batch, moduli)
+    np.testing.assert_array_equal(mfhe.to_host_u64(c[0]), ocr)
+    np.testing.assert_array_equal(mfhe.to_host_u64(c[1]), oci)
+    inv = [orc.L.orc_invmod(2 ** 35 % q, q) for q in moduli[:3]] + [0] * (L - 3) if L > 3 else \
+        [orc.L.orc_invmod(2 ** 35 % q, q) for q in moduli[:L]]
+    ctx.trace_rescale(c[0], c[1], n, L, batch, inv)
+    torch.cuda.synchronize()
+    osr, osi = orc.trace_rescale(ocr, oci, n, L, batch, moduli, inv)
+    np.testing.assert_array_equal(mfhe.to_host_u64(c[0]), osr)
+    np.testing.assert_array_equal(mfhe.to_host_u64(c[1]), osi)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("n,L,batch", [(64, 11, 16), (64, 3, 1), (128, 2, 3), (8, 11, 4), (2, 1, 5)])
+def test_trace_reference_moduli_vs_oracle(mfhe, orc, n, L, batch):
+    """n = 64 / 128 take the FP64 tile kernel (KR = 16), n = 8 / 2 the u128 kernel."""
+    _gpu_case(mfhe, orc, RNS, 6, n, L, batch, n * 100 + L)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("bits", [49, 58])
+def test_trace_wide_moduli_vs_oracle(mfhe, orc, bits):
+    """49-bit primes: FP64 kernel with KR = 2; 58-bit primes: the u128 kernel."""
+    moduli = orc.gen_primes(bits, 1 << 8, 4)
+    _gpu_case(mfhe, orc, moduli, 6, 64, 4, 3, bits)
+
+
+@pytest.mark.gpu
+def test_trace_invalid_arguments(mfhe):
+    import torch
+    ctx = mfhe.Context(RNS, 6, mfhe.CONV_PHANTOM)
+    t = torch.zeros(64 * 64, dtype=torch.int64, device="cuda")
+    with pytest.raises(mfhe.MfheError):
+        ctx.trace_gemm(t, t, t, t, t, t, 48, 1, 1)        # n not a power of two
+    with pytest.raises(mfhe.MfheError):
+        ctx.trace_gemm(t, t, t, t, t, t, 64, 12, 1)       # more limbs than the context
+    with pytest.raises(mfhe.MfheError):
+        ctx.trace_map_bprime(t, t, t, t, 64, 1, 1)        # aliasing output
