@@ -203,7 +203,7 @@ def trace_line(reps=10):
         ctx.trace_rescale(c[0], c[1], n, L, batch, inv)
     full()
     torch.cuda.synchronize()
-    e = [torch.cuda.Event(enable_timing=True) for _ in range(4)]
+    e = [torch.cuda.Event(enable_timing=True) for _ in range(5)]
     e[0].record()
     for _ in range(reps):
         gemm()
@@ -211,14 +211,24 @@ def trace_line(reps=10):
     for _ in range(reps):
         full()
     e[2].record()
+    ctx.set_option(mfhe.OPT_TRACE_SPLIT, 0)
+    gemm()
+    e[3].record()
+    for _ in range(reps):
+        gemm()
+    e[4].record()
     torch.cuda.synchronize()
+    ctx.set_option(mfhe.OPT_TRACE_SPLIT, 1)
     g_ms, f_ms = e[0].elapsed_time(e[1]) / reps, e[1].elapsed_time(e[2]) / reps
+    m_ms = e[3].elapsed_time(e[4]) / reps
     macs = batch * L * n ** 3
     ctx.close()
     return {"workload": "batched trace GEMM, 512 matrices x L=11 x n=64 complex mod q (reference geometry)",
             "gemm_ms": round(g_ms, 3), "map_gemm_rescale_ms": round(f_ms, 3),
             "complex_modmac_per_s": round(macs / (g_ms * 1e-3)),
-            "fp64_valu_tflops_est": round(macs * 4 * 6 / (g_ms * 1e-3) / 1e12, 1)}
+            "kernel": "split-digit FP64 FMA (16 FMA per complex MAC)",
+            "fp64_tflops": round(macs * 16 * 2 / (g_ms * 1e-3) / 1e12, 1), "fp64_peak_tflops": 78.6,
+            "modmul_kernel_gemm_ms": round(m_ms, 3)}
 
 
 def cpu_baseline(log_n, moduli, seconds):

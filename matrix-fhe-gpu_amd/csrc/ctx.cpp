@@ -573,6 +573,10 @@ extern "C" int mfhe_ctx_set_option(mfhe_ctx* c, int opt, int64_t v) {
             if (v < 0 || v > 1) return set_error(MFHE_EINVAL, "he fused must be 0 or 1");
             c->he_fused = (int)v;
             return MFHE_OK;
+        case MFHE_OPT_TRACE_SPLIT:
+            if (v < 0 || v > 1) return set_error(MFHE_EINVAL, "trace split must be 0 or 1");
+            c->trace_split = (int)v;
+            return MFHE_OK;
         case MFHE_OPT_CRT_WORDS:
             if (v < 1 || v > 32) return set_error(MFHE_EINVAL, "crt words must be in [1, 32]");
             if (v <= c->W) return MFHE_OK;
@@ -611,6 +615,7 @@ extern "C" int mfhe_ctx_get_option(const mfhe_ctx* c, int opt, int64_t* v) {
         case MFHE_OPT_WCRT_MFMA: *v = c->d_wVdig ? c->wcrt_mfma : 0; return MFHE_OK;
         case MFHE_OPT_CGEMM_MFMA: *v = c->cgemm_mfma; return MFHE_OK;
         case MFHE_OPT_HE_FUSED: *v = c->he_fused; return MFHE_OK;
+        case MFHE_OPT_TRACE_SPLIT: *v = c->trace_split; return MFHE_OK;
         case MFHE_OPT_NTT_FUSED_LAG: *v = c->ntt_fused_lag; return MFHE_OK;
         case MFHE_OPT_NTT_FUSED_ERRORS: {
             // synchronous: the error word of the last fused launch (0 = no spin timed out)

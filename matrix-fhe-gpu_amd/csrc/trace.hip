@@ -14,6 +14,8 @@
 // thread, the reference's order of operations with a Barrett reduction in place of %).
 #include <hip/hip_runtime.h>
 
+#include <cmath>
+
 #include "mfhe_ctx.hpp"
 
 namespace mfhe {
@@ -126,7 +128,7 @@ __global__ __launch_bounds__(256) void trace_gemm_f64_kernel(
         }
         __syncthreads();
     }
-    const double nm = nmod[l];   // n mod q, centred
+    const double nm = nmod[3 * l];   // n mod q, centred
 #pragma unroll
     for (int i = 0; i < 4; ++i)
 #pragma unroll
@@ -134,6 +136,112 @@ __global__ __launch_bounds__(256) void trace_gemm_f64_kernel(
             const uint64_t o = base + (uint64_t)(tm * TR_TILE + ty + 16 * i) * n + tn * TR_TILE + tx + 16 * j;
             Cr[o] = ar.canon(ar.mulmod(ar.reduce(accr[i][j]), nm));
             Ci[o] = ar.canon(ar.mulmod(ar.reduce(acci[i][j]), nm));
+        }
+}
+
+// Split-digit variant (every q < 2^45): each centred operand is cut as x = x1 2^S + x0 with x0 centred in
+// [-2^(S-1), 2^(S-1)] (S = ceil(bits(q_max) / 2)), so every digit product is an exact FP64 value <= 2^(bits-1)
+// and a complex MAC is 16 plain FMAs into three exact accumulators per part (hi = x1 y1, mid = x1 y0 + x0 y1,
+// lo = x0 y0) instead of four error-free modmuls (~28 ops).  |partial sums| <= 4 * 64 * 2^44 < 2^53 over any
+// 64 k; the accumulators are reduced mod q every 64 k (n > 64) and folded in the epilogue as
+// C = n (hi 2^2S + mid 2^S + lo) mod q with per-limb centred constants c1 = 2^S, c2 = 2^2S mod q.
+// 512 threads per 64 x 64 tile, 4 x 2 outputs per thread (48 accumulator doubles).
+__global__ __launch_bounds__(512) void trace_gemm_split_kernel(
+    const uint64_t* __restrict__ Ar, const uint64_t* __restrict__ Ai, const uint64_t* __restrict__ Br,
+    const uint64_t* __restrict__ Bi, uint64_t* __restrict__ Cr, uint64_t* __restrict__ Ci,
+    const LimbConst* __restrict__ lf, const double* __restrict__ consts, int log_n, int L, double two_s,
+    double inv_two_s) {
+    // [re hi, re lo, im hi, im lo][k][row]
+    __shared__ double sA[4][TR_KP][TR_LDS];
+    __shared__ double sB[4][TR_KP][TR_LDS];
+    const int n = 1 << log_n, tdim = n / TR_TILE, tiles = tdim * tdim;
+    const uint64_t mat = blockIdx.x / tiles;
+    const int tile = blockIdx.x % tiles, tm = tile / tdim, tn = tile % tdim;
+    const int l = (int)(mat % (uint64_t)L);
+    const ArithF64 ar(lf[l]);
+    const double q = ar.q, qh = 0.5 * q;
+    const uint64_t base = mat << (2 * log_n);
+    const uint64_t* src[4] = {Ar + base + (uint64_t)(tm * TR_TILE) * n, Ai + base + (uint64_t)(tm * TR_TILE) * n,
+                              Br + base + (uint64_t)(tn * TR_TILE) * n, Bi + base + (uint64_t)(tn * TR_TILE) * n};
+    const int tid = threadIdx.x, tx = tid & 31, ty = tid >> 5;
+
+    double hr[4][2], mr[4][2], lr[4][2], hi[4][2], mi[4][2], li[4][2];
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+#pragma unroll
+        for (int j = 0; j < 2; ++j) hr[i][j] = mr[i][j] = lr[i][j] = hi[i][j] = mi[i][j] = li[i][j] = 0.0;
+
+    for (int k0 = 0; k0 < n; k0 += TR_KP) {
+#pragma unroll
+        for (int e = 0; e < 2; ++e) {
+            const int idx = tid + 512 * e, r = idx >> 4, kk = idx & 15;
+            const uint64_t g = (uint64_t)r * n + k0 + kk;
+#pragma unroll
+            for (int m = 0; m < 4; ++m) {
+                double v = ArithF64::from_u64(src[m][g]);
+                v = v > qh ? v - q : v;
+                const double d1 = ArithF64::round_int(v, inv_two_s);
+                const double d0 = __fma_rn(-d1, two_s, v);
+                double(*dst)[TR_KP][TR_LDS] = m < 2 ? sA : sB;
+                dst[2 * (m & 1)][kk][r] = d1;
+                dst[2 * (m & 1) + 1][kk][r] = d0;
+            }
+        }
+        __syncthreads();
+#pragma unroll 2
+        for (int kk = 0; kk < TR_KP; ++kk) {
+            double a1r[4], a0r[4], a1i[4], a0i[4], b1r[2], b0r[2], b1i[2], b0i[2];
+#pragma unroll
+            for (int i = 0; i < 4; ++i) {
+                a1r[i] = sA[0][kk][ty + 16 * i];
+                a0r[i] = sA[1][kk][ty + 16 * i];
+                a1i[i] = sA[2][kk][ty + 16 * i];
+                a0i[i] = sA[3][kk][ty + 16 * i];
+            }
+#pragma unroll
+            for (int j = 0; j < 2; ++j) {
+                b1r[j] = sB[0][kk][tx + 32 * j];
+                b0r[j] = sB[1][kk][tx + 32 * j];
+                b1i[j] = sB[2][kk][tx + 32 * j];
+                b0i[j] = sB[3][kk][tx + 32 * j];
+            }
+#pragma unroll
+            for (int i = 0; i < 4; ++i)
+#pragma unroll
+                for (int j = 0; j < 2; ++j) {
+                    hr[i][j] = __fma_rn(a1r[i], b1r[j], __fma_rn(-a1i[i], b1i[j], hr[i][j]));
+                    lr[i][j] = __fma_rn(a0r[i], b0r[j], __fma_rn(-a0i[i], b0i[j], lr[i][j]));
+                    mr[i][j] = __fma_rn(a1r[i], b0r[j], __fma_rn(a0r[i], b1r[j], mr[i][j]));
+                    mr[i][j] = __fma_rn(-a1i[i], b0i[j], __fma_rn(-a0i[i], b1i[j], mr[i][j]));
+                    hi[i][j] = __fma_rn(a1r[i], b1i[j], __fma_rn(a1i[i], b1r[j], hi[i][j]));
+                    li[i][j] = __fma_rn(a0r[i], b0i[j], __fma_rn(a0i[i], b0r[j], li[i][j]));
+                    mi[i][j] = __fma_rn(a1r[i], b0i[j], __fma_rn(a0r[i], b1i[j], mi[i][j]));
+                    mi[i][j] = __fma_rn(a1i[i], b0r[j], __fma_rn(a0i[i], b1r[j], mi[i][j]));
+                }
+        }
+        __syncthreads();
+        if (((k0 + TR_KP) & 63) == 0 && k0 + TR_KP < n) {
+#pragma unroll
+            for (int i = 0; i < 4; ++i)
+#pragma unroll
+                for (int j = 0; j < 2; ++j) {
+                    hr[i][j] = ar.reduce(hr[i][j]); mr[i][j] = ar.reduce(mr[i][j]); lr[i][j] = ar.reduce(lr[i][j]);
+                    hi[i][j] = ar.reduce(hi[i][j]); mi[i][j] = ar.reduce(mi[i][j]); li[i][j] = ar.reduce(li[i][j]);
+                }
+        }
+    }
+    const double nm = consts[3 * l], c1 = consts[3 * l + 1], c2 = consts[3 * l + 2];   // centred n, 2^S, 2^2S mod q
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+#pragma unroll
+        for (int j = 0; j < 2; ++j) {
+            const uint64_t o = base + (uint64_t)(tm * TR_TILE + ty + 16 * i) * n + tn * TR_TILE + tx + 32 * j;
+            const double vr = ar.mulmod(ar.reduce(hr[i][j]), c2) + ar.mulmod(ar.reduce(mr[i][j]), c1) +
+                              ar.reduce(lr[i][j]);
+            const double vi = ar.mulmod(ar.reduce(hi[i][j]), c2) + ar.mulmod(ar.reduce(mi[i][j]), c1) +
+                              ar.reduce(li[i][j]);
+            Cr[o] = ar.canon(ar.mulmod(ar.reduce(vr), nm));
+            Ci[o] = ar.canon(ar.mulmod(ar.reduce(vi), nm));
         }
 }
 
@@ -228,23 +336,39 @@ extern "C" int mfhe_trace_gemm(mfhe_ctx* c, const uint64_t* ar, const uint64_t* 
     const uint64_t total = (uint64_t)batch * nlimbs * n * n;
     const int log_n = ilog2(n);
     if (c->f64_ok && n % TR_TILE == 0) {
-        if (!c->d_trace_nmod || c->trace_n != n) {   // n mod q_l, centred, per limb (rebuilt when n changes)
-            if (!c->d_trace_nmod) {
-                MFHE_HIP(hipMalloc(&c->d_trace_nmod, sizeof(double) * c->L));
-                c->allocs.push_back(c->d_trace_nmod);
-            }
-            std::vector<double> nm(c->L);
-            for (int l = 0; l < c->L; ++l) {
-                const uint64_t q = c->moduli[l], v = (uint64_t)n % q;
-                nm[l] = v > q / 2 ? (double)v - (double)q : (double)v;
-            }
-            MFHE_HIP(hipMemcpy(c->d_trace_nmod, nm.data(), sizeof(double) * c->L, hipMemcpyHostToDevice));
-            c->trace_n = n;
-        }
         uint64_t qmax = 0;
         for (int l = 0; l < nlimbs; ++l) qmax = c->moduli[l] > qmax ? c->moduli[l] : qmax;
+        const int qbits = 64 - __builtin_clzll(qmax);
+        const int S = (qbits + 1) / 2;
+        const bool split = c->trace_split && qbits <= 45;
+        if (!c->d_trace_nmod || c->trace_n != n || c->trace_s != S) {
+            // per limb, centred: n mod q, 2^S mod q, 2^2S mod q (rebuilt when n or S changes)
+            if (!c->d_trace_nmod) {
+                MFHE_HIP(hipMalloc(&c->d_trace_nmod, sizeof(double) * 3 * c->L));
+                c->allocs.push_back(c->d_trace_nmod);
+            }
+            auto centred = [](uint64_t v, uint64_t q) { return v > q / 2 ? (double)v - (double)q : (double)v; };
+            std::vector<double> k(3 * c->L);
+            for (int l = 0; l < c->L; ++l) {
+                const uint64_t q = c->moduli[l];
+                const uint64_t t1 = (uint64_t)(((unsigned __int128)1 << S) % q);
+                k[3 * l] = centred((uint64_t)n % q, q);
+                k[3 * l + 1] = centred(t1, q);
+                k[3 * l + 2] = centred((uint64_t)((unsigned __int128)t1 * t1 % q), q);
+            }
+            MFHE_HIP(hipMemcpy(c->d_trace_nmod, k.data(), sizeof(double) * 3 * c->L, hipMemcpyHostToDevice));
+            c->trace_n = n;
+            c->trace_s = S;
+        }
         const uint64_t blocks = (uint64_t)batch * nlimbs * (n / TR_TILE) * (n / TR_TILE);
         if (blocks > 0x7fffffffull) return set_error(MFHE_EINVAL, "mfhe_trace_gemm: batch too large");
+        if (split) {
+            hipLaunchKernelGGL(trace_gemm_split_kernel, dim3((uint32_t)blocks), dim3(512), 0, (hipStream_t)s, ar, ai,
+                               bpr, bpi, cr, ci, c->d_limbs, c->d_trace_nmod, log_n, nlimbs, std::ldexp(1.0, S),
+                               std::ldexp(1.0, -S));
+            MFHE_CHECK_LAUNCH("trace_gemm_split_kernel");
+            return MFHE_OK;
+        }
         if ((double)qmax * 48.5 < 9007199254740992.0)   // (0.5 + 3 * 16) q < 2^53
             hipLaunchKernelGGL(trace_gemm_f64_kernel<16>, dim3((uint32_t)blocks), dim3(256), 0, (hipStream_t)s, ar,
                                ai, bpr, bpi, cr, ci, c->d_limbs, c->d_trace_nmod, log_n, nlimbs);

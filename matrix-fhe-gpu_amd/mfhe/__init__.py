@@ -25,7 +25,7 @@ CONV_PHANTOM, CONV_GL, CONV_WCRT = 1, 2, 4
 ARITH_AUTO, ARITH_F64, ARITH_U64 = 0, 1, 2
 OPT_NTT_CHUNK_BYTES, OPT_NTT_PLAN, OPT_CRT_WORDS, OPT_NTT_WG_PER_CU, OPT_NTT_PREFETCH = 1, 2, 3, 4, 5
 OPT_NTT_FUSED, OPT_NTT_FUSED_LAG, OPT_NTT_FUSED_ERRORS, OPT_WCRT_MFMA = 6, 7, 8, 9
-OPT_CGEMM_MFMA, OPT_HE_FUSED = 10, 11
+OPT_CGEMM_MFMA, OPT_HE_FUSED, OPT_TRACE_SPLIT = 10, 11, 12
 
 #: reference parameters (include/core/config.h:7-52)
 RNS_MODULI = [

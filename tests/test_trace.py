@@ -59,9 +59,10 @@ def test_oracle_trace_matches_python_integers(orc):
         np.testing.assert_array_equal(sr.reshape(batch, L, -1)[:, l], v.astype(np.uint64))
 
 
-def _gpu_case(mfhe, orc, moduli, log_n_ctx, n, L, batch, seed):
+def _gpu_case(mfhe, orc, moduli, log_n_ctx, n, L, batch, seed, split=1):
     import torch
     ctx = mfhe.Context(moduli, log_n_ctx, mfhe.CONV_PHANTOM)
+    ctx.set_option(mfhe.OPT_TRACE_SPLIT, split)
     rng = np.random.default_rng(seed)
     ar, ai, br, bi = (_rand(rng, batch, L, n, moduli) for _ in range(4))
     d = [mfhe.to_device_u64(x) for x in (ar, ai, br, bi)]
@@ -86,16 +87,37 @@ def _gpu_case(mfhe, orc, moduli, log_n_ctx, n, L, batch, seed):
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("n,L,batch", [(64, 11, 16), (64, 3, 1), (128, 2, 3), (8, 11, 4), (2, 1, 5)])
-def test_trace_reference_moduli_vs_oracle(mfhe, orc, n, L, batch):
-    """n = 64 / 128 take the FP64 tile kernel (KR = 16), n = 8 / 2 the u128 kernel."""
-    _gpu_case(mfhe, orc, RNS, 6, n, L, batch, n * 100 + L)
+@pytest.mark.parametrize("split", [1, 0])
+@pytest.mark.parametrize("n,L,batch", [(64, 11, 16), (64, 3, 1), (128, 2, 3), (256, 1, 1), (8, 11, 4), (2, 1, 5)])
+def test_trace_reference_moduli_vs_oracle(mfhe, orc, n, L, batch, split):
+    """n = 64 / 128 / 256: the split-digit FMA kernel (split = 1; n > 64 crosses its 64-k reductions) or the
+    modmul tile kernel (KR = 16); n = 8 / 2: the u128 kernel."""
+    _gpu_case(mfhe, orc, RNS, 6, n, L, batch, n * 100 + L, split)
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("bits", [49, 58])
+def test_trace_split_extreme_operands(mfhe, orc):
+    """Split kernel at its digit bounds: every operand q - 1 or (q - 1) / 2 (largest centred magnitudes)."""
+    import torch
+    n, L, batch = 128, 11, 2
+    ctx = mfhe.Context(RNS, 6, mfhe.CONV_PHANTOM)
+    q = np.array(RNS, np.uint64)[None, :, None]
+    hi = np.broadcast_to(q - 1, (batch, L, n * n)).ravel().copy()
+    half = np.broadcast_to((q - 1) // 2, (batch, L, n * n)).ravel().copy()
+    for ar, ai, br, bi in ((hi, hi, hi, hi), (half, half, half, half), (hi, half, half, hi)):
+        d = [mfhe.to_device_u64(x) for x in (ar, ai, br, bi)]
+        c = [torch.empty_like(d[0]), torch.empty_like(d[0])]
+        ctx.trace_gemm(d[0], d[1], d[2], d[3], c[0], c[1], n, L, batch)
+        torch.cuda.synchronize()
+        ocr, oci = orc.trace_gemm(ar, ai, br, bi, n, L, batch, RNS)
+        np.testing.assert_array_equal(mfhe.to_host_u64(c[0]), ocr)
+        np.testing.assert_array_equal(mfhe.to_host_u64(c[1]), oci)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("bits", [40, 45, 49, 58])
 def test_trace_wide_moduli_vs_oracle(mfhe, orc, bits):
-    """49-bit primes: FP64 kernel with KR = 2; 58-bit primes: the u128 kernel."""
+    """40 / 45-bit primes: split kernel (S = 20 / 23); 49-bit: modmul kernel with KR = 2; 58-bit: u128."""
     moduli = orc.gen_primes(bits, 1 << 8, 4)
     _gpu_case(mfhe, orc, moduli, 6, 64, 4, 3, bits)
 
