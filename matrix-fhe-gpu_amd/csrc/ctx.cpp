@@ -574,7 +574,7 @@ extern "C" int mfhe_ctx_set_option(mfhe_ctx* c, int opt, int64_t v) {
             c->he_fused = (int)v;
             return MFHE_OK;
         case MFHE_OPT_TRACE_SPLIT:
-            if (v < 0 || v > 1) return set_error(MFHE_EINVAL, "trace split must be 0 or 1");
+            if (v < 0 || v > 2) return set_error(MFHE_EINVAL, "trace split must be 0, 1 or 2");
             c->trace_split = (int)v;
             return MFHE_OK;
         case MFHE_OPT_CRT_WORDS:

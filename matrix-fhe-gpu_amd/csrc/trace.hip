@@ -245,6 +245,133 @@ __global__ __launch_bounds__(512) void trace_gemm_split_kernel(
         }
 }
 
+// The same split-digit product on the FP64 matrix cores (v_mfma_f64_16x16x4_f64): every digit product and
+// partial sum is an exact integer below 2^53, so the MFMA's fused sums are exact too.  512 threads per
+// 64 x 64 tile; wave w owns rows 16 (w >> 1) .. +16 and columns 32 (w & 1) .. +32 as two 16 x 16 blocks,
+// each with six accumulators (hi / mid / lo for the real and imaginary parts): 16 MFMAs per block per
+// 4-deep k-step.  LDS: [plane][row][k] with a 17-double row pitch (fragment loads spread over the banks).
+// Fragment maps (f64 16x16x4): A lane l = A[l & 15][k = l >> 4], B lane l = B[k = l >> 4][l & 15],
+// C/D reg g of lane l = C[(l >> 4) + 4 g][l & 15].
+typedef double tr_v4d __attribute__((ext_vector_type(4)));
+constexpr int TR_CAP = TR_KP + 1;
+
+__global__ __launch_bounds__(512) void trace_gemm_split_mfma_kernel(
+    const uint64_t* __restrict__ Ar, const uint64_t* __restrict__ Ai, const uint64_t* __restrict__ Br,
+    const uint64_t* __restrict__ Bi, uint64_t* __restrict__ Cr, uint64_t* __restrict__ Ci,
+    const LimbConst* __restrict__ lf, const double* __restrict__ consts, int log_n, int L, double two_s,
+    double inv_two_s) {
+    // planes: 0 re hi, 1 re lo, 2 im hi, 3 im lo
+    __shared__ double sA[4][TR_TILE * TR_CAP];
+    __shared__ double sB[4][TR_TILE * TR_CAP];
+    const int n = 1 << log_n, tdim = n / TR_TILE, tiles = tdim * tdim;
+    const uint64_t mat = blockIdx.x / tiles;
+    const int tile = blockIdx.x % tiles, tm = tile / tdim, tn = tile % tdim;
+    const int l = (int)(mat % (uint64_t)L);
+    const ArithF64 ar(lf[l]);
+    const double q = ar.q, qh = 0.5 * q;
+    const uint64_t base = mat << (2 * log_n);
+    const uint64_t* src[4] = {Ar + base + (uint64_t)(tm * TR_TILE) * n, Ai + base + (uint64_t)(tm * TR_TILE) * n,
+                              Br + base + (uint64_t)(tn * TR_TILE) * n, Bi + base + (uint64_t)(tn * TR_TILE) * n};
+    const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+    const int wm = (w >> 1) * 16, wp = (w & 1) * 32, r = lane & 15, kq = lane >> 4;
+
+    // acc[j][0..5] = hr, mr, lr, hi, mi, li of block j
+    tr_v4d acc[2][6];
+#pragma unroll
+    for (int j = 0; j < 2; ++j)
+#pragma unroll
+        for (int t = 0; t < 6; ++t) acc[j][t] = tr_v4d{0, 0, 0, 0};
+
+    for (int k0 = 0; k0 < n; k0 += TR_KP) {
+#pragma unroll
+        for (int e = 0; e < 2; ++e) {
+            const int idx = tid + 512 * e, row = idx >> 4, kk = idx & 15;
+            const uint64_t g = (uint64_t)row * n + k0 + kk;
+#pragma unroll
+            for (int m = 0; m < 4; ++m) {
+                double v = ArithF64::from_u64(src[m][g]);
+                v = v > qh ? v - q : v;
+                const double d1 = ArithF64::round_int(v, inv_two_s);
+                const double d0 = __fma_rn(-d1, two_s, v);
+                double(*dst)[TR_TILE * TR_CAP] = m < 2 ? sA : sB;
+                dst[2 * (m & 1)][row * TR_CAP + kk] = d1;
+                dst[2 * (m & 1) + 1][row * TR_CAP + kk] = d0;
+            }
+        }
+        __syncthreads();
+#pragma unroll
+        for (int ks = 0; ks < TR_KP / 4; ++ks) {
+            const int k = ks * 4 + kq;
+            const int ao = (wm + r) * TR_CAP + k;
+            const double a1r = sA[0][ao], a0r = sA[1][ao], a1i = sA[2][ao], a0i = sA[3][ao];
+            const double n1i = -a1i, n0i = -a0i;
+            double b1r[2], b0r[2], b1i[2], b0i[2];
+#pragma unroll
+            for (int j = 0; j < 2; ++j) {
+                const int bo = (wp + 16 * j + r) * TR_CAP + k;
+                b1r[j] = sB[0][bo];
+                b0r[j] = sB[1][bo];
+                b1i[j] = sB[2][bo];
+                b0i[j] = sB[3][bo];
+            }
+#define TR_MF(acc_, x_, y_) acc_ = __builtin_amdgcn_mfma_f64_16x16x4f64(x_, y_, acc_, 0, 0, 0)
+            // interleave the twelve accumulators so no MFMA waits on the previous one
+#pragma unroll
+            for (int j = 0; j < 2; ++j) {
+                TR_MF(acc[j][0], a1r, b1r[j]);
+                TR_MF(acc[j][1], a1r, b0r[j]);
+                TR_MF(acc[j][2], a0r, b0r[j]);
+                TR_MF(acc[j][3], a1r, b1i[j]);
+                TR_MF(acc[j][4], a1r, b0i[j]);
+                TR_MF(acc[j][5], a0r, b0i[j]);
+            }
+#pragma unroll
+            for (int j = 0; j < 2; ++j) {
+                TR_MF(acc[j][0], n1i, b1i[j]);
+                TR_MF(acc[j][1], a0r, b1r[j]);
+                TR_MF(acc[j][2], n0i, b0i[j]);
+                TR_MF(acc[j][3], a1i, b1r[j]);
+                TR_MF(acc[j][4], a0r, b1i[j]);
+                TR_MF(acc[j][5], a0i, b0r[j]);
+            }
+#pragma unroll
+            for (int j = 0; j < 2; ++j) {
+                TR_MF(acc[j][1], n1i, b0i[j]);
+                TR_MF(acc[j][4], a1i, b0r[j]);
+            }
+#pragma unroll
+            for (int j = 0; j < 2; ++j) {
+                TR_MF(acc[j][1], n0i, b1i[j]);
+                TR_MF(acc[j][4], a0i, b1r[j]);
+            }
+#undef TR_MF
+        }
+        __syncthreads();
+        if (((k0 + TR_KP) & 63) == 0 && k0 + TR_KP < n) {
+#pragma unroll
+            for (int j = 0; j < 2; ++j)
+#pragma unroll
+                for (int t = 0; t < 6; ++t)
+#pragma unroll
+                    for (int g = 0; g < 4; ++g) acc[j][t][g] = ar.reduce(acc[j][t][g]);
+        }
+    }
+    const double nm = consts[3 * l], c1 = consts[3 * l + 1], c2 = consts[3 * l + 2];
+#pragma unroll
+    for (int j = 0; j < 2; ++j)
+#pragma unroll
+        for (int g = 0; g < 4; ++g) {
+            const uint64_t o =
+                base + (uint64_t)(tm * TR_TILE + wm + kq + 4 * g) * n + tn * TR_TILE + wp + 16 * j + r;
+            const double vr = ar.mulmod(ar.reduce(acc[j][0][g]), c2) + ar.mulmod(ar.reduce(acc[j][1][g]), c1) +
+                              ar.reduce(acc[j][2][g]);
+            const double vi = ar.mulmod(ar.reduce(acc[j][3][g]), c2) + ar.mulmod(ar.reduce(acc[j][4][g]), c1) +
+                              ar.reduce(acc[j][5][g]);
+            Cr[o] = ar.canon(ar.mulmod(ar.reduce(vr), nm));
+            Ci[o] = ar.canon(ar.mulmod(ar.reduce(vi), nm));
+        }
+}
+
 // Any q < 2^62, any n: one output per thread, the reference's sequence (batched_trace.cu:124-144).
 __global__ void trace_gemm_u128_kernel(const uint64_t* __restrict__ Ar, const uint64_t* __restrict__ Ai,
                                        const uint64_t* __restrict__ Br, const uint64_t* __restrict__ Bi,
@@ -362,6 +489,13 @@ extern "C" int mfhe_trace_gemm(mfhe_ctx* c, const uint64_t* ar, const uint64_t* 
         }
         const uint64_t blocks = (uint64_t)batch * nlimbs * (n / TR_TILE) * (n / TR_TILE);
         if (blocks > 0x7fffffffull) return set_error(MFHE_EINVAL, "mfhe_trace_gemm: batch too large");
+        if (split && c->trace_split == 2) {
+            hipLaunchKernelGGL(trace_gemm_split_mfma_kernel, dim3((uint32_t)blocks), dim3(512), 0, (hipStream_t)s, ar,
+                               ai, bpr, bpi, cr, ci, c->d_limbs, c->d_trace_nmod, log_n, nlimbs, std::ldexp(1.0, S),
+                               std::ldexp(1.0, -S));
+            MFHE_CHECK_LAUNCH("trace_gemm_split_mfma_kernel");
+            return MFHE_OK;
+        }
         if (split) {
             hipLaunchKernelGGL(trace_gemm_split_kernel, dim3((uint32_t)blocks), dim3(512), 0, (hipStream_t)s, ar, ai,
                                bpr, bpi, cr, ci, c->d_limbs, c->d_trace_nmod, log_n, nlimbs, std::ldexp(1.0, S),

@@ -87,11 +87,12 @@ def _gpu_case(mfhe, orc, moduli, log_n_ctx, n, L, batch, seed, split=1):
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("split", [1, 0])
+@pytest.mark.parametrize("split", [2, 1, 0])
 @pytest.mark.parametrize("n,L,batch", [(64, 11, 16), (64, 3, 1), (128, 2, 3), (256, 1, 1), (8, 11, 4), (2, 1, 5)])
 def test_trace_reference_moduli_vs_oracle(mfhe, orc, n, L, batch, split):
-    """n = 64 / 128 / 256: the split-digit FMA kernel (split = 1; n > 64 crosses its 64-k reductions) or the
-    modmul tile kernel (KR = 16); n = 8 / 2: the u128 kernel."""
+    """n = 64 / 128 / 256: the split-digit kernel on the FP64 matrix cores (split = 2) or as VALU FMAs
+    (split = 1; n > 64 crosses their 64-k reductions), or the modmul tile kernel (split = 0, KR = 16);
+    n = 8 / 2: the u128 kernel."""
     _gpu_case(mfhe, orc, RNS, 6, n, L, batch, n * 100 + L, split)
 
 
@@ -104,7 +105,9 @@ def test_trace_split_extreme_operands(mfhe, orc):
     q = np.array(RNS, np.uint64)[None, :, None]
     hi = np.broadcast_to(q - 1, (batch, L, n * n)).ravel().copy()
     half = np.broadcast_to((q - 1) // 2, (batch, L, n * n)).ravel().copy()
-    for ar, ai, br, bi in ((hi, hi, hi, hi), (half, half, half, half), (hi, half, half, hi)):
+    for split, (ar, ai, br, bi) in [(m, x) for m in (1, 2)
+                                    for x in ((hi, hi, hi, hi), (half, half, half, half), (hi, half, half, hi))]:
+        ctx.set_option(mfhe.OPT_TRACE_SPLIT, split)
         d = [mfhe.to_device_u64(x) for x in (ar, ai, br, bi)]
         c = [torch.empty_like(d[0]), torch.empty_like(d[0])]
         ctx.trace_gemm(d[0], d[1], d[2], d[3], c[0], c[1], n, L, batch)
@@ -116,10 +119,11 @@ def test_trace_split_extreme_operands(mfhe, orc):
 
 @pytest.mark.gpu
 @pytest.mark.parametrize("bits", [40, 45, 49, 58])
-def test_trace_wide_moduli_vs_oracle(mfhe, orc, bits):
-    """40 / 45-bit primes: split kernel (S = 20 / 23); 49-bit: modmul kernel with KR = 2; 58-bit: u128."""
+@pytest.mark.parametrize("split", [2, 1])
+def test_trace_wide_moduli_vs_oracle(mfhe, orc, bits, split):
+    """40 / 45-bit primes: split kernels (S = 20 / 23); 49-bit: modmul kernel with KR = 2; 58-bit: u128."""
     moduli = orc.gen_primes(bits, 1 << 8, 4)
-    _gpu_case(mfhe, orc, moduli, 6, 64, 4, 3, bits)
+    _gpu_case(mfhe, orc, moduli, 6, 128, 4, 3, bits, split)
 
 
 @pytest.mark.gpu
