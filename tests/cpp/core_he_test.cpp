@@ -7,7 +7,9 @@
 #include "HE.cuh"
 #include "batched_encoder.cuh"
 #include "config.h"
+#include "batched_trace.cuh"
 #include "encoder.cuh"
+#include "trace.cuh"
 #include "test_util.hpp"
 
 using namespace matrix_fhe;
@@ -153,6 +155,54 @@ int main() {
         for (auto* c : {&c1r, &c1i, &c2r, &c2i}) free_ciphertext(*c);
         hipFree(sk.data); hipFree(dm1); hipFree(dm2); hipFree(dout);
         hipFree(e1r); hipFree(e1i); hipFree(e2r); hipFree(e2i);
+    }
+
+    // ---- batched trace GEMM (batched_trace.cu:37-197): map B -> B', C = n A B'^T, rescale ----
+    std::printf("[trace gemm]\n");
+    {
+        const int batch = 2;
+        const size_t tw = (size_t)batch * L * n2;
+        std::vector<uint64_t> hA[2], hB[2];
+        for (int c = 0; c < 2; ++c) {
+            hA[c].resize(tw);
+            hB[c].resize(tw);
+            for (size_t i = 0; i < tw; ++i) {
+                const uint64_t q = RNS_MODULI[(i / n2) % L];
+                hA[c][i] = splitmix(seed) % q;
+                hB[c][i] = splitmix(seed) % q;
+            }
+        }
+        uint64_t *ar = h2d(hA[0]), *ai = h2d(hA[1]), *br = h2d(hB[0]), *bi = h2d(hB[1]);
+        uint64_t *bpr = dev_alloc<uint64_t>(tw), *bpi = dev_alloc<uint64_t>(tw);
+        uint64_t *cr = dev_alloc<uint64_t>(tw), *ci = dev_alloc<uint64_t>(tw);
+        map_B_to_Bprime_batched(br, bi, bpr, bpi, n, L, batch);
+        trace_gemm_batched(ar, ai, bpr, bpi, cr, ci, n, L, batch);
+        auto gr = d2h(cr, tw), gi = d2h(ci, tw);
+        const uint64_t inv0 = 3, inv1 = 5, inv2 = 7;
+        rescale_by_delta_batched(cr, ci, n, L, batch, inv0, inv1, inv2);
+        auto sr = d2h(cr, tw), si = d2h(ci, tw);
+        size_t bad = 0;
+        for (size_t o = 0; o < tw; o += 131) {
+            const size_t mat = o / n2, pos = o % n2, row = pos / n, col = pos % n, l = mat % L;
+            const uint64_t q = RNS_MODULI[l];
+            uint64_t accr = 0, acci = 0;
+            for (int t = 0; t < n; ++t) {   // B'[col][t] from B: row j = (n - col) mod n, conj, times -i if j != 0
+                const size_t j = (n - col) % n, src = mat * n2 + j * n + t;
+                const uint64_t b_r = hB[0][src], b_i = hB[1][src];
+                const uint64_t nbr = b_r ? q - b_r : 0, nbi = b_i ? q - b_i : 0;
+                const uint64_t pr = j == 0 ? b_r : nbi, pi = j == 0 ? nbi : nbr;
+                const uint64_t a_r = hA[0][mat * n2 + row * n + t], a_i = hA[1][mat * n2 + row * n + t];
+                accr = (accr + mulmod(a_r, pr, q) + q - mulmod(a_i, pi, q)) % q;
+                acci = (acci + mulmod(a_r, pi, q) + mulmod(a_i, pr, q)) % q;
+            }
+            accr = mulmod(accr, n % q, q);
+            acci = mulmod(acci, n % q, q);
+            bad += gr[o] != accr || gi[o] != acci;
+            const uint64_t inv = l == 0 ? inv0 : l == 1 ? inv1 : l == 2 ? inv2 : 0;   // limbs >= 3: times 0
+            bad += sr[o] != mulmod(accr, inv, q) || si[o] != mulmod(acci, inv, q);
+        }
+        EXPECT(bad == 0, "trace gemm / rescale mismatches %zu", bad);
+        for (auto* p : {ar, ai, br, bi, bpr, bpi, cr, ci}) hipFree(p);
     }
 
     bool threw = false;
