@@ -203,7 +203,7 @@ def trace_line(reps=10):
         ctx.trace_rescale(c[0], c[1], n, L, batch, inv)
     full()
     torch.cuda.synchronize()
-    e = [torch.cuda.Event(enable_timing=True) for _ in range(7)]
+    e = [torch.cuda.Event(enable_timing=True) for _ in range(9)]
     e[0].record()
     for _ in range(reps):
         gemm()
@@ -226,12 +226,23 @@ def trace_line(reps=10):
     torch.cuda.synchronize()
     ctx.set_option(mfhe.OPT_TRACE_SPLIT, 2)
     x_ms = e[5].elapsed_time(e[6]) / reps
+
+    def fused():
+        ctx.trace_product(planes[0], planes[1], planes[2], planes[3], c[0], c[1], n, L, batch, inv)
+    fused()
+    e[7].record()
+    for _ in range(reps):
+        fused()
+    e[8].record()
+    torch.cuda.synchronize()
+    p_ms = e[7].elapsed_time(e[8]) / reps
     g_ms, f_ms = e[0].elapsed_time(e[1]) / reps, e[1].elapsed_time(e[2]) / reps
     m_ms = e[3].elapsed_time(e[4]) / reps
     macs = batch * L * n ** 3
     ctx.close()
     return {"workload": "batched trace GEMM, 512 matrices x L=11 x n=64 complex mod q (reference geometry)",
             "gemm_ms": round(g_ms, 3), "map_gemm_rescale_ms": round(f_ms, 3),
+            "fused_product_ms": round(p_ms, 3),
             "complex_modmac_per_s": round(macs / (g_ms * 1e-3)),
             "kernel": "split-digit product on v_mfma_f64_16x16x4 (16 MFMA per 16x16x4 complex block-step, exact)",
             "fp64_tflops": round(macs * 16 * 2 / (g_ms * 1e-3) / 1e12, 1), "fp64_peak_tflops": 78.6,

@@ -255,11 +255,18 @@ __global__ __launch_bounds__(512) void trace_gemm_split_kernel(
 typedef double tr_v4d __attribute__((ext_vector_type(4)));
 constexpr int TR_CAP = TR_KP + 1;
 
+struct TracePost {
+    double f[64];   // per limb, centred: n * inv[l] mod q_l (fused product)
+};
+
+// FUSE: the B -> B' map is applied while staging (B' row p = f(B row (n - p) mod n)) and the rescale is
+// folded into the epilogue constant (mfhe_trace_product); otherwise B' is read as given.
+template <bool FUSE>
 __global__ __launch_bounds__(512) void trace_gemm_split_mfma_kernel(
     const uint64_t* __restrict__ Ar, const uint64_t* __restrict__ Ai, const uint64_t* __restrict__ Br,
     const uint64_t* __restrict__ Bi, uint64_t* __restrict__ Cr, uint64_t* __restrict__ Ci,
     const LimbConst* __restrict__ lf, const double* __restrict__ consts, int log_n, int L, double two_s,
-    double inv_two_s) {
+    double inv_two_s, TracePost post) {
     // planes: 0 re hi, 1 re lo, 2 im hi, 3 im lo
     __shared__ double sA[4][TR_TILE * TR_CAP];
     __shared__ double sB[4][TR_TILE * TR_CAP];
@@ -287,12 +294,30 @@ __global__ __launch_bounds__(512) void trace_gemm_split_mfma_kernel(
         for (int e = 0; e < 2; ++e) {
             const int idx = tid + 512 * e, row = idx >> 4, kk = idx & 15;
             const uint64_t g = (uint64_t)row * n + k0 + kk;
+            double v[4];
+            if (FUSE) {   // map_Bprime_batched_kernel (batched_trace.cu:57-77) on the fly
+                const int j = (n - (tn * TR_TILE + row)) & (n - 1);
+                const uint64_t gb = base + (uint64_t)j * n + k0 + kk;
+                v[0] = ArithF64::from_u64(src[0][g]);
+                v[1] = ArithF64::from_u64(src[1][g]);
+                v[2] = ArithF64::from_u64(Br[gb]);
+                v[3] = ArithF64::from_u64(Bi[gb]);
+#pragma unroll
+                for (int m = 0; m < 4; ++m) v[m] = v[m] > qh ? v[m] - q : v[m];
+                const double br0 = v[2], bi0 = v[3];
+                v[2] = j == 0 ? br0 : -bi0;   // conj, then times -i for rows j != 0
+                v[3] = j == 0 ? -bi0 : -br0;
+            } else {
+#pragma unroll
+                for (int m = 0; m < 4; ++m) {
+                    v[m] = ArithF64::from_u64(src[m][g]);
+                    v[m] = v[m] > qh ? v[m] - q : v[m];
+                }
+            }
 #pragma unroll
             for (int m = 0; m < 4; ++m) {
-                double v = ArithF64::from_u64(src[m][g]);
-                v = v > qh ? v - q : v;
-                const double d1 = ArithF64::round_int(v, inv_two_s);
-                const double d0 = __fma_rn(-d1, two_s, v);
+                const double d1 = ArithF64::round_int(v[m], inv_two_s);
+                const double d0 = __fma_rn(-d1, two_s, v[m]);
                 double(*dst)[TR_TILE * TR_CAP] = m < 2 ? sA : sB;
                 dst[2 * (m & 1)][row * TR_CAP + kk] = d1;
                 dst[2 * (m & 1) + 1][row * TR_CAP + kk] = d0;
@@ -356,7 +381,7 @@ __global__ __launch_bounds__(512) void trace_gemm_split_mfma_kernel(
                     for (int g = 0; g < 4; ++g) acc[j][t][g] = ar.reduce(acc[j][t][g]);
         }
     }
-    const double nm = consts[3 * l], c1 = consts[3 * l + 1], c2 = consts[3 * l + 2];
+    const double nm = FUSE ? post.f[l] : consts[3 * l], c1 = consts[3 * l + 1], c2 = consts[3 * l + 2];
 #pragma unroll
     for (int j = 0; j < 2; ++j)
 #pragma unroll
@@ -490,9 +515,9 @@ extern "C" int mfhe_trace_gemm(mfhe_ctx* c, const uint64_t* ar, const uint64_t* 
         const uint64_t blocks = (uint64_t)batch * nlimbs * (n / TR_TILE) * (n / TR_TILE);
         if (blocks > 0x7fffffffull) return set_error(MFHE_EINVAL, "mfhe_trace_gemm: batch too large");
         if (split && c->trace_split == 2) {
-            hipLaunchKernelGGL(trace_gemm_split_mfma_kernel, dim3((uint32_t)blocks), dim3(512), 0, (hipStream_t)s, ar,
-                               ai, bpr, bpi, cr, ci, c->d_limbs, c->d_trace_nmod, log_n, nlimbs, std::ldexp(1.0, S),
-                               std::ldexp(1.0, -S));
+            hipLaunchKernelGGL(trace_gemm_split_mfma_kernel<false>, dim3((uint32_t)blocks), dim3(512), 0,
+                               (hipStream_t)s, ar, ai, bpr, bpi, cr, ci, c->d_limbs, c->d_trace_nmod, log_n, nlimbs,
+                               std::ldexp(1.0, S), std::ldexp(1.0, -S), TracePost{});
             MFHE_CHECK_LAUNCH("trace_gemm_split_mfma_kernel");
             return MFHE_OK;
         }
@@ -533,5 +558,52 @@ extern "C" int mfhe_trace_rescale(mfhe_ctx* c, uint64_t* cr, uint64_t* ci, int n
     hipLaunchKernelGGL(trace_rescale_kernel, g1(total), dim3(256), 0, (hipStream_t)s, cr, ci, c->d_rns_mu, a,
                        2 * ilog2(n), nlimbs, total);
     MFHE_CHECK_LAUNCH("trace_rescale_kernel");
+    return MFHE_OK;
+}
+
+extern "C" int mfhe_trace_product(mfhe_ctx* c, const uint64_t* ar, const uint64_t* ai, const uint64_t* br,
+                                  const uint64_t* bi, uint64_t* cr, uint64_t* ci, int n, int nlimbs, size_t batch,
+                                  const uint64_t* inv, mfhe_stream_t s) {
+    if (int rc = trace_check(c, n, nlimbs, batch, "mfhe_trace_product")) return rc;
+    if (!ar || !ai || !br || !bi || !cr || !ci) return set_error(MFHE_EINVAL, "mfhe_trace_product: null pointer");
+    if (cr == br || cr == bi || ci == br || ci == bi)
+        return set_error(MFHE_EINVAL, "mfhe_trace_product: output must not alias B");
+    uint64_t qmax = 0;
+    for (int l = 0; l < nlimbs; ++l) qmax = c->moduli[l] > qmax ? c->moduli[l] : qmax;
+    if (!c->f64_ok || n % TR_TILE != 0 || 64 - __builtin_clzll(qmax) > 45 || nlimbs > 64)
+        return set_error(MFHE_EUNSUPPORTED, "mfhe_trace_product: needs n % 64 == 0, every q < 2^45, nlimbs <= 64 "
+                                            "(use mfhe_trace_map_bprime + mfhe_trace_gemm + mfhe_trace_rescale)");
+    // per-limb constants for this n and digit split (same table as mfhe_trace_gemm)
+    const int qbits = 64 - __builtin_clzll(qmax), S = (qbits + 1) / 2;
+    if (!c->d_trace_nmod || c->trace_n != n || c->trace_s != S) {
+        if (!c->d_trace_nmod) {
+            MFHE_HIP(hipMalloc(&c->d_trace_nmod, sizeof(double) * 3 * c->L));
+            c->allocs.push_back(c->d_trace_nmod);
+        }
+        auto centred = [](uint64_t v, uint64_t q) { return v > q / 2 ? (double)v - (double)q : (double)v; };
+        std::vector<double> k(3 * c->L);
+        for (int l = 0; l < c->L; ++l) {
+            const uint64_t q = c->moduli[l];
+            const uint64_t t1 = (uint64_t)(((unsigned __int128)1 << S) % q);
+            k[3 * l] = centred((uint64_t)n % q, q);
+            k[3 * l + 1] = centred(t1, q);
+            k[3 * l + 2] = centred((uint64_t)((unsigned __int128)t1 * t1 % q), q);
+        }
+        MFHE_HIP(hipMemcpy(c->d_trace_nmod, k.data(), sizeof(double) * 3 * c->L, hipMemcpyHostToDevice));
+        c->trace_n = n;
+        c->trace_s = S;
+    }
+    TracePost post{};
+    for (int l = 0; l < nlimbs; ++l) {
+        const uint64_t q = c->moduli[l], nm = (uint64_t)n % q;
+        const uint64_t f = inv ? (uint64_t)((unsigned __int128)nm * (inv[l] % q) % q) : nm;
+        post.f[l] = f > q / 2 ? (double)f - (double)q : (double)f;
+    }
+    const uint64_t blocks = (uint64_t)batch * nlimbs * (n / TR_TILE) * (n / TR_TILE);
+    if (blocks > 0x7fffffffull) return set_error(MFHE_EINVAL, "mfhe_trace_product: batch too large");
+    hipLaunchKernelGGL(trace_gemm_split_mfma_kernel<true>, dim3((uint32_t)blocks), dim3(512), 0, (hipStream_t)s, ar,
+                       ai, br, bi, cr, ci, c->d_limbs, c->d_trace_nmod, ilog2(n), nlimbs, std::ldexp(1.0, S),
+                       std::ldexp(1.0, -S), post);
+    MFHE_CHECK_LAUNCH("trace_gemm_split_mfma_kernel<fused>");
     return MFHE_OK;
 }

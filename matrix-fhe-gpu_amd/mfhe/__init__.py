@@ -106,6 +106,7 @@ _sig("mfhe_ct_mul_tensor", [_vp] * 7)
 _sig("mfhe_trace_map_bprime", [_vp] * 5 + [ctypes.c_int, ctypes.c_int, _sz, _vp])
 _sig("mfhe_trace_gemm", [_vp] * 7 + [ctypes.c_int, ctypes.c_int, _sz, _vp])
 _sig("mfhe_trace_rescale", [_vp] * 3 + [ctypes.c_int, ctypes.c_int, _sz, _u64p, _vp])
+_sig("mfhe_trace_product", [_vp] * 7 + [ctypes.c_int, ctypes.c_int, _sz, _u64p, _vp])
 _sig("mfhe_ctx_reserve_workspace", [_vp])
 _sig("mfhe_encode", [_vp, _vp, _vp, _vp, _vp])
 _sig("mfhe_decode", [_vp, _vp, _vp, _vp, _vp])
@@ -301,6 +302,10 @@ class Context:
         arr = (ctypes.c_uint64 * nlimbs)(*[int(v) for v in inv[:nlimbs]])
         check(lib.mfhe_trace_rescale(self._h, _ptr(c_re), _ptr(c_im), n, nlimbs, batch, arr, _stream_ptr(stream)),
               "trace_rescale")
+    def trace_product(self, a_re, a_im, b_re, b_im, c_re, c_im, n, nlimbs, batch, inv=None, stream=None):
+        arr = (ctypes.c_uint64 * nlimbs)(*[int(v) for v in inv[:nlimbs]]) if inv is not None else None
+        check(lib.mfhe_trace_product(self._h, _ptr(a_re), _ptr(a_im), _ptr(b_re), _ptr(b_im), _ptr(c_re), _ptr(c_im),
+                                     n, nlimbs, batch, arr, _stream_ptr(stream)), "trace_product")
     def xy_dft(self, src, dst, lanes, stream=None):
         check(lib.mfhe_xy_dft(self._h, _ptr(src), _ptr(dst), lanes, _stream_ptr(stream)), "xy_dft"); return dst
     def xy_idft(self, src, dst, lanes, stream=None):

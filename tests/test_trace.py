@@ -137,3 +137,39 @@ def test_trace_invalid_arguments(mfhe):
         ctx.trace_gemm(t, t, t, t, t, t, 64, 12, 1)       # more limbs than the context
     with pytest.raises(mfhe.MfheError):
         ctx.trace_map_bprime(t, t, t, t, 64, 1, 1)        # aliasing output
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("n,L,batch,rescale", [(64, 11, 8, True), (64, 11, 3, False), (128, 3, 2, True),
+                                               (256, 1, 1, True)])
+def test_trace_product_fused_vs_oracle(mfhe, orc, n, L, batch, rescale):
+    """mfhe_trace_product (map + GEMM + rescale in one launch) == the oracle's three stages."""
+    import torch
+    ctx = mfhe.Context(RNS, 6, mfhe.CONV_PHANTOM)
+    rng = np.random.default_rng(n + L)
+    ar, ai, br, bi = (_rand(rng, batch, L, n, RNS) for _ in range(4))
+    d = [mfhe.to_device_u64(x) for x in (ar, ai, br, bi)]
+    c = [torch.empty_like(d[0]), torch.empty_like(d[0])]
+    inv = ([orc.L.orc_invmod(2 ** 35 % q, q) for q in RNS[:min(L, 3)]] + [0] * max(0, L - 3)) if rescale else None
+    ctx.trace_product(d[0], d[1], d[2], d[3], c[0], c[1], n, L, batch, inv)
+    torch.cuda.synchronize()
+    obpr, obpi = orc.trace_map_bprime(br, bi, n, L, batch, RNS)
+    ocr, oci = orc.trace_gemm(ar, ai, obpr, obpi, n, L, batch, RNS)
+    if rescale:
+        ocr, oci = orc.trace_rescale(ocr, oci, n, L, batch, RNS, inv)
+    np.testing.assert_array_equal(mfhe.to_host_u64(c[0]), ocr)
+    np.testing.assert_array_equal(mfhe.to_host_u64(c[1]), oci)
+
+
+@pytest.mark.gpu
+def test_trace_product_unsupported_shapes(mfhe, orc):
+    import torch
+    t = torch.zeros(2 * 64 * 64, dtype=torch.int64, device="cuda")
+    o = torch.zeros_like(t)
+    ctx = mfhe.Context(orc.gen_primes(58, 1 << 8, 2), 6, mfhe.CONV_PHANTOM)
+    with pytest.raises(mfhe.MfheError) as e:
+        ctx.trace_product(t, t, t, t, o, o, 64, 2, 1)
+    assert e.value.code == mfhe.EUNSUPPORTED
+    ctx2 = mfhe.Context(RNS, 6, mfhe.CONV_PHANTOM)
+    with pytest.raises(mfhe.MfheError):
+        ctx2.trace_product(t, t, t, t, o, o, 32, 2, 1)
