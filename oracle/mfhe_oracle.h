@@ -163,6 +163,16 @@ void orc_trace_gemm(const uint64_t* Ar, const uint64_t* Ai, const uint64_t* Br, 
 void orc_trace_rescale(uint64_t* Cr, uint64_t* Ci, int n, int L, size_t batch, const uint64_t* moduli,
                        const uint64_t* inv);
 
+/* ---------------- synthetic inputs ----------------
+ * Not a reference function: the deterministic input generator shared by tests/golden/make_digests.py
+ * and the full-shape GPU parity tests, so both sides see identical inputs.  Element i of a
+ * [npoly][L][N] batch (i counted from poly `poly0`) is splitmix64(seed + i) mod q_l; message i is
+ * splitmix64(seed + i) mapped to a double in [-1, 1) (53 random bits). */
+uint64_t orc_splitmix64(uint64_t x);
+void orc_fill_residues(uint64_t* out, size_t npoly, int L, size_t N, const uint64_t* moduli, uint64_t seed,
+                       size_t poly0);
+void orc_fill_messages(double* out, size_t count, uint64_t seed, size_t idx0);
+
 #ifdef __cplusplus
 }
 #endif

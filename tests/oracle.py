@@ -88,6 +88,23 @@ _s("orc_he_VinvT", [vp], vp)
 _s("orc_trace_map_bprime", [vp, vp, vp, vp, ci, ci, sz, vp])
 _s("orc_trace_gemm", [vp, vp, vp, vp, vp, vp, ci, ci, sz, vp])
 _s("orc_trace_rescale", [vp, vp, ci, ci, sz, vp, vp])
+_s("orc_splitmix64", [u64], u64)
+_s("orc_fill_residues", [vp, sz, ci, sz, vp, u64, sz])
+_s("orc_fill_messages", [vp, sz, u64, sz])
+
+
+def fill_residues(npoly: int, L_: int, N: int, moduli, seed: int, poly0: int = 0) -> np.ndarray:
+    """Deterministic synthetic residues [npoly][L][N] (orc_fill_residues; SURVEY.md §8(d) seeds)."""
+    out = np.empty(npoly * L_ * N, np.uint64)
+    L.orc_fill_residues(P(out), npoly, L_, N, P(U64(moduli)), seed, poly0)
+    return out
+
+
+def fill_messages(count: int, seed: int, idx0: int = 0) -> np.ndarray:
+    """Deterministic messages in [-1, 1) (orc_fill_messages)."""
+    out = np.empty(count, np.float64)
+    L.orc_fill_messages(P(out), count, seed, idx0)
+    return out
 
 
 def P(a: np.ndarray):
