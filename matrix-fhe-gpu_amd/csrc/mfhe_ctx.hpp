@@ -76,7 +76,9 @@ struct mfhe_ctx {
     int num_cus = 256;
     int ntt_fused = 0;       // N = 2^15..2^17: both passes in one launch (MFHE_OPT_NTT_FUSED)
     int ntt_fused_lag = 2;   // pass-2 lag in polynomials per XCD queue
-    void* fused_buf = nullptr;   // FusedSync + map/arr arrays, grown on demand
+    void* fused_buf = nullptr;   // FusedSync + arrival arrays, grown on demand
+    int xcc_nq = 0;              // fused NTT: XCDs found by the census (0 = not run yet)
+    uint8_t xcc_qmap[16] = {};   // XCC id -> fused queue index
     int8_t* d_wVdig = nullptr;   // [L][wD][512][512] balanced base-256 digits of V   (i8 MFMA W-CRT)
     int8_t* d_wVidig = nullptr;  // same for V^-1
     uint64_t* d_wrtab = nullptr; // [L][2 wD - 1][2] (256^s mod q, Shoup)

@@ -1,57 +1,65 @@
 // ntt_fused.hpp -- both passes of a two-pass NTT (N = 2^15..2^17) in one launch, with the intermediate
 // handed from pass 1 to pass 2 inside the XCD's L2.
 //
-// Why: the two-pass plan moves every element through the memory side four times (read + write per
-// pass; rocprofv3 FETCH/WRITE_SIZE = 2.03x the algorithmic bytes, profiles/r01_pmc_ntt_traffic.json).
-// Here the K tiles of pass 1 of a polynomial and the K tiles of its pass 2 are tasks of one per-XCD
-// queue, so pass 2 reads what pass 1 of the same XCD just wrote, out of that XCD's L2.
+// Why: the two-pass plan moves every element through the L2 <-> fabric path four times (read + write per
+// pass; rocprofv3 FETCH/WRITE_SIZE = 2.01x the algorithmic bytes, profiles/r01_pmc_ntt_traffic.json), and
+// that path, not the ALU, is what bounds it.  Here pass 2 of a polynomial re-reads the intermediate from
+// the L2 of the XCD whose workgroups just wrote it, so the fabric sees 24N bytes per transform, not 32N.
 //
-// Scheduling.  Workgroups read their XCD id (HW_REG_XCC_ID) and pull task numbers from that XCD's
-// queue head.  Task t of XCD x: block k = t / 2K, u = t % 2K;  u < K is pass-1 tile u of local poly
-// k, u >= K is pass-2 tile u - K of local poly k - D (lag D lets pass 1 finish before pass 2 needs
-// it).  Local poly j of XCD x is bound to the next global (limb, batch) polynomial by whoever pulls
-// its tile 0 (a device-wide counter), so XCDs load-balance and no XCD count is assumed.
-// Deadlock freedom: a task only ever waits for tasks with smaller numbers of the same queue, and
-// those were pulled by running workgroups that never wait on later tasks.  Every spin is bounded;
-// a timeout sets FusedSync::err (read by mfhe_ctx_get_option(MFHE_OPT_NTT_FUSED_ERRORS)).
+// Scheduling.  One task queue per XCD (queue index from HW_REG_XCC_ID through the census map built at
+// context creation).  Queue x owns the global polynomials g = j*Q + x (j = its local polynomial index), so
+// no binding has to be published.  Task t of a queue: block k = t / 2K, u = t % 2K; u < K is pass-1 tile u
+// of local poly k, u >= K is pass-2 tile u - K of local poly k - D (lag D).  A workgroup fetches the number
+// of its NEXT task while it works on the current one, so the dequeue atomic is off the critical path.
 //
-// Visibility.  Producer and consumer of a hand-off always sit on the same XCD (the queue is chosen by
-// HW_REG_XCC_ID, never by blockIdx), so the XCD's L2 is the coherence point between them and the
-// intermediate never has to leave it (MI355X_MICROARCH.md "inter-workgroup visibility": stores keep
-// their lines in the XCD L2; only the CU's own L1 can be stale).  Producer: plain stores -> every wave
-// s_waitcnt vmcnt(0) (stores acknowledged by the L2) -> barrier -> lane 0 relaxed agent atomic add on the
-// poly's arrival counter.  Consumer: lane 0 polls the counter with sc1 (L1-bypass) loads -> barrier ->
-// every load of the intermediate is an sc1 load, served by the L2, so no L1 line of this CU (e.g. the
-// original input it read in pass 1) can be returned.  No agent release/acquire fence is needed: the
-// release's L2 write-back (buffer_wbl2) is exactly the traffic this kernel exists to avoid.
+// Forward progress does not depend on which workgroups are resident.  Pass-1 tasks never wait.  A pass-2
+// task waits only for the K pass-1 tiles of its polynomial, all of which have smaller task numbers of the
+// same queue.  By induction the smallest-numbered unfinished task is always being executed by the running
+// workgroup that dequeued it (a workgroup's prefetched task has a larger number than its current one), so
+// it finishes.  Only running workgroups dequeue.  Should an XCD get no workgroup at all, its queue is
+// drained at the end by the last workgroup to leave (exit counter), which then runs both passes itself.
+//
+// Visibility.  Producer and consumer of a hand-off sit on the same XCD (the queue is chosen by XCC id, never
+// by blockIdx), so that XCD's L2 is the coherence point.  Producer: plain stores (they keep the line in the
+// L2) -> every wave s_waitcnt vmcnt(0) -> barrier -> lane 0 relaxed agent atomic add on the poly's arrival
+// counter.  That signal is deferred until the workgroup's next tile has issued its loads, and it is always
+// sent before the workgroup waits for anything, so the progress argument above still holds.  Consumer: lane 0 polls the counter (relaxed agent loads bypass L1) -> barrier -> every load of
+// the intermediate is an sc1 load, served by the L2, so no stale L1 line of this CU can be returned.
+// Final outputs are stored sc1 nt: they leave the L2 at once and do not evict intermediates.
 #pragma once
 #include "ntt_kernels.hpp"
 
+#ifndef MFHE_FUSED_CPOL_IN
+#define MFHE_FUSED_CPOL_IN 0        // pass-1 input loads
+#endif
+#ifndef MFHE_FUSED_CPOL_MID_LD
+#define MFHE_FUSED_CPOL_MID_LD 16   // pass-2 intermediate loads: sc1 (L1 bypass) is required
+#endif
+
 namespace mfhe {
 
-constexpr int kFusedXcc = 16;    // queue slots (XCC ids 0..15)
+constexpr int kFusedXcc = 16;    // HW_REG_XCC_ID values 0..15
 
-// Zeroed before every launch.  map / arr hold `cap` entries per XCD queue (one per local poly, no
-// reuse), cap >= npl + the empty local polys workgroups can open before they exit.
+// Zeroed before every launch.
 struct FusedSync {
     uint32_t head[kFusedXcc][32];   // one 128-B line per queue head
-    uint32_t gcount;                // next global polynomial
-    uint32_t err;                   // 1: map wait timed out, 2: arrival wait timed out, 4: cap exceeded
+    uint32_t exits;                 // workgroups that left the main loop
+    uint32_t err;                   // 2: an arrival wait timed out (a bug; the tile was skipped)
     uint32_t pad[30];
-    // followed by uint64_t map[kFusedXcc][cap] ((local poly + 1) << 32 | global poly)
-    //         and uint32_t arr[kFusedXcc][cap] (pass-1 arrivals)
+    // followed by uint32_t arr[kFusedXcc][cap]: pass-1 arrivals per local polynomial
 };
 
 template <class TS>
 struct FusedArgs {
     PassArgs<TS> p;        // shared by pass 1 and pass 2 (forward: column then block; inverse: block then column)
     FusedSync* sync;
-    uint64_t* map;
     uint32_t* arr;
-    uint32_t cap;          // entries per XCD in map / arr
+    uint32_t cap;          // local polynomials per queue (entries of arr per queue)
     uint32_t K;            // tiles per polynomial in each pass
     uint32_t npl;          // polynomials (batch * nlimbs)
     uint32_t lag;          // D
+    uint32_t nq;           // queues = XCDs found by the census
+    uint8_t qmap[kFusedXcc];   // XCC id -> queue (0xFF: unseen id -> queue 0)
 };
 
 __device__ __forceinline__ uint32_t xcc_id() {
@@ -60,14 +68,16 @@ __device__ __forceinline__ uint32_t xcc_id() {
     return x & (kFusedXcc - 1);
 }
 
-__device__ __forceinline__ uint64_t ld_agent(const uint64_t* p) {
-    return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-}
 __device__ __forceinline__ uint32_t ld_agent(const uint32_t* p) {
     return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
 
-constexpr uint32_t kSpinLimit = 1u << 24;
+constexpr uint32_t kSpinLimit = 1u << 26;
+
+// Census: which XCC ids exist (bit i of *mask set by a workgroup running on XCC i).
+static __global__ void xcc_census_kernel(uint32_t* mask) {
+    if (threadIdx.x == 0) atomicOr(mask, 1u << xcc_id());
+}
 
 template <class P1, class P2, class TS>
 __global__ __launch_bounds__(P1::NT) void ntt_fused_kernel(FusedArgs<TS> f) {
@@ -76,91 +86,87 @@ __global__ __launch_bounds__(P1::NT) void ntt_fused_kernel(FusedArgs<TS> f) {
     constexpr size_t LDSW = (P1::LDS_BYTES > P2::LDS_BYTES ? P1::LDS_BYTES : P2::LDS_BYTES) / 8;
     uint32_t* bc = reinterpret_cast<uint32_t*>(lds + LDSW);   // broadcast words
     const uint32_t t = threadIdx.x;
-    const uint32_t x = xcc_id();
     FusedSync* sy = f.sync;
-    const uint32_t K = f.K, D = f.lag;
+    const uint32_t K = f.K, D = f.lag, Q = f.nq;
     const P1 p1(f.p);
     const P2 p2(f.p);
 
+    // Pass-1 arrival of local poly `p` (queue q): every wave's stores drained, then one counter add.  Deferred
+    // to the next task's loads so no workgroup idles on its own store acknowledgements.
+    constexpr uint32_t kNone = 0xFFFFFFFFu;
+    uint32_t pend = kNone;
+    uint32_t q = 0;
+    auto flush = [&](uint32_t p) {
+        if (p == kNone) return;
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        __syncthreads();
+        if (t == 0) __hip_atomic_fetch_add(&f.arr[(size_t)q * f.cap + p], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    };
+    q = f.qmap[xcc_id()];
+    if (q >= Q) q = 0;
+    bool drain = false;   // last workgroup out: draining queues nobody ran
     while (true) {
-        __syncthreads();   // previous task's readers of bc[] are done
-        if (t == 0) {
-            const uint32_t task = __hip_atomic_fetch_add(&sy->head[x][0], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        // local polys of queue q and its task count
+        const uint32_t nloc = q < f.npl ? (f.npl - q + Q - 1) / Q : 0;
+        const uint32_t total = (nloc + D) * 2 * K;
+        if (t == 0) bc[0] = __hip_atomic_fetch_add(&sy->head[q][0], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        __syncthreads();
+        uint32_t task = __builtin_amdgcn_readfirstlane(bc[0]);
+        while (task < total) {
+            // prefetch the next task number; lane 0 publishes it at the end of this task
+            uint32_t nxt = 0;
+            if (t == 0) nxt = __hip_atomic_fetch_add(&sy->head[q][0], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
             const uint32_t k = task / (2 * K), u = task % (2 * K);
-            uint32_t kind = 0, j = 0, tile = 0, v = 0xFFFFFFFFu;   // kind: 0 skip, 1 pass 1, 2 pass 2, 3 exit
-            uint64_t* const map = f.map + (size_t)x * f.cap;
-            uint32_t* const arr = f.arr + (size_t)x * f.cap;
-            if (k >= f.cap) {
-                // more local polys than provisioned: every real poly was handed out long before this
-                atomicOr(&sy->err, 4u);
-                kind = 3;
-            } else if (u < K) {
-                j = k;
-                tile = u;
-                uint64_t* slot = &map[j];
-                const uint64_t tag = (uint64_t)(j + 1) << 32;
-                if (tile == 0) {
-                    v = __hip_atomic_fetch_add(&sy->gcount, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-                    __hip_atomic_store(slot, tag | v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-                } else {
-                    uint32_t n = 0;
-                    uint64_t m;
-                    while (((m = ld_agent(slot)) >> 32) != (uint64_t)(j + 1)) {
-                        __builtin_amdgcn_s_sleep(1);
-                        if (++n == kSpinLimit) { atomicOr(&sy->err, 1u); break; }
-                    }
-                    v = (uint32_t)m;
+            if (u < K) {
+                if (k < nloc) {
+                    const uint32_t g = k * Q + q;
+                    const TileLoc L = p1.locate(g * K + u);
+                    uint64_t raw[P1::R];
+                    p1.template load_pol<MFHE_FUSED_CPOL_IN>(L, raw);
+                    flush(pend);   // the previous tile's stores drained behind this tile's loads
+                    pend = k;
+                    p1.compute_store(L, raw, lds);
                 }
-                kind = v < f.npl ? 1 : 0;
             } else if (k >= D) {
-                j = k - D;
-                tile = u - K;
-                const uint64_t* slot = &map[j];
-                uint32_t n = 0;
-                uint64_t m;
-                while (((m = ld_agent(slot)) >> 32) != (uint64_t)(j + 1)) {
-                    __builtin_amdgcn_s_sleep(1);
-                    if (++n == kSpinLimit) { atomicOr(&sy->err, 1u); break; }
-                }
-                v = (uint32_t)m;
-                if (v >= f.npl) {
-                    kind = 3;
-                } else {
-                    n = 0;
-                    while (ld_agent(&arr[j]) < K) {
-                        __builtin_amdgcn_s_sleep(1);
+                const uint32_t j = k - D;
+                flush(pend);   // never wait while holding an unsignalled tile
+                pend = kNone;
+                if (t == 0) {
+                    uint32_t n = 0;
+                    while (ld_agent(&f.arr[(size_t)q * f.cap + j]) < K) {
+                        __builtin_amdgcn_s_sleep(2);
                         if (++n == kSpinLimit) { atomicOr(&sy->err, 2u); break; }
                     }
-                    kind = 2;
+                    bc[1] = n == kSpinLimit;
+                }
+                __syncthreads();
+                if (!__builtin_amdgcn_readfirstlane(bc[1])) {
+                    const uint32_t g = j * Q + q;
+                    const TileLoc L = p2.locate(g * K + (u - K));
+                    uint64_t raw[P2::R];
+                    p2.template load_pol<MFHE_FUSED_CPOL_MID_LD>(L, raw);
+                    p2.compute_store(L, raw, lds);
                 }
             }
-            bc[0] = kind;
-            bc[1] = v * K + tile;   // tile number inside the pass
-            bc[2] = j;
-        }
-        __syncthreads();
-        // readfirstlane: the broadcast words are workgroup-uniform, so tile addressing stays in SGPRs
-        const uint32_t kind = __builtin_amdgcn_readfirstlane(bc[0]);
-        const uint32_t lb = __builtin_amdgcn_readfirstlane(bc[1]);
-        const uint32_t j = __builtin_amdgcn_readfirstlane(bc[2]);
-        if (kind == 3) break;
-        if (kind == 0) continue;
-        if (kind == 1) {
-            const TileLoc L = p1.locate(lb);
-            uint64_t raw[P1::R];
-            p1.load(L, raw);
-            p1.compute_store(L, raw, lds);
-            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+            __syncthreads();   // readers of bc[] (and of the LDS tile) are done
+            if (t == 0) bc[0] = nxt;
             __syncthreads();
-            if (t == 0) {
-                __hip_atomic_fetch_add(&f.arr[(size_t)x * f.cap + j], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-            }
-        } else {
-            const TileLoc L = p2.locate(lb);
-            uint64_t raw[P2::R];
-            p2.load_l2(L, raw);
-            p2.compute_store(L, raw, lds);
+            task = __builtin_amdgcn_readfirstlane(bc[0]);
         }
+        flush(pend);
+        pend = kNone;
+        if (drain) {
+            if (++q >= Q) break;
+            continue;
+        }
+        // leave; the last workgroup out drains every queue that still has tasks (an XCD with no workgroup)
+        __syncthreads();
+        if (t == 0) bc[2] = __hip_atomic_fetch_add(&sy->exits, 1u, __ATOMIC_ACQ_REL, __HIP_MEMORY_SCOPE_AGENT);
+        __syncthreads();
+        if (__builtin_amdgcn_readfirstlane(bc[2]) != gridDim.x - 1) break;
+        drain = true;
+        q = 0;
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
     }
 }
 

@@ -28,6 +28,19 @@
 
 #include "ntt_arith.hpp"
 
+#ifndef MFHE_NTT_CPOL_IN
+#define MFHE_NTT_CPOL_IN 0
+#endif
+#ifndef MFHE_NTT_CPOL_OUT
+#define MFHE_NTT_CPOL_OUT 18   // sc1 nt: final outputs leave the L2 at once (+2-3% two-pass, profiles/r02_cpol.txt)
+#endif
+#ifndef MFHE_NTT_CPOL_MID_LD
+#define MFHE_NTT_CPOL_MID_LD 0
+#endif
+#ifndef MFHE_NTT_CPOL_MID_ST
+#define MFHE_NTT_CPOL_MID_ST 0
+#endif
+
 namespace mfhe {
 
 struct TwSrcF {
@@ -172,22 +185,37 @@ struct NttPass {
     __device__ __forceinline__ TileLoc locate(uint32_t lb) const {
         return tile_loc<LOG_G, NG, COLS, UNI>(a.data, a.batch, a.nl, a.start_limb, a.logN, s0, lb, gl);
     }
+    // cache policy (gfx950 CPol bits: 1 sc0, 2 nt, 16 sc1) of the global loads / stores of a pass:
+    // input of a transform, intermediate between the passes, output of a transform
+    static constexpr int kCpolLd = IN_RAW ? MFHE_NTT_CPOL_MID_LD : MFHE_NTT_CPOL_IN;
+    static constexpr int kCpolSt = OUT_RAW ? MFHE_NTT_CPOL_MID_ST : MFHE_NTT_CPOL_OUT;
+
     __device__ __forceinline__ void load(const TileLoc& L, uint64_t (&raw)[R]) const {
+        if constexpr (UNI && kCpolLd != 0) {
+            const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(L.base, 0, 0x7FFFFFFF, 0x00020000);
 #pragma unroll
-        for (int k = 0; k < R; ++k) raw[k] = L.base[jidx(L, Gm::g_of(r_load, tau, k))];
+            for (int k = 0; k < R; ++k)
+                raw[k] = __builtin_bit_cast(uint64_t, __builtin_amdgcn_raw_buffer_load_b64(
+                                                          rs, (int)(jidx(L, Gm::g_of(r_load, tau, k)) * 8u), 0, kCpolLd));
+        } else {
+#pragma unroll
+            for (int k = 0; k < R; ++k) raw[k] = L.base[jidx(L, Gm::g_of(r_load, tau, k))];
+        }
     }
 
-    // L1-bypass (sc1) loads, served by the XCD's L2: reads data another CU of this XCD just stored.
-    // Buffer loads off the workgroup-uniform tile base (UNI plans): SGPR descriptor + 32-bit lane offset.
-    __device__ __forceinline__ void load_l2(const TileLoc& L, uint64_t (&raw)[R]) const {
-        static_assert(UNI, "load_l2 needs a workgroup-uniform tile base");
-        constexpr int kSc1 = 16;   // CPol::SC1 (gfx940+ cache-policy bits)
+    // Loads with an explicit cache policy (CPol aux bits) off the workgroup-uniform tile base (UNI plans):
+    // SGPR buffer descriptor + 32-bit lane offset.  The fused kernel reads the intermediate with sc1
+    // (L1 bypass, served by the XCD's L2: data another CU of this XCD just stored).
+    template <int CPOL>
+    __device__ __forceinline__ void load_pol(const TileLoc& L, uint64_t (&raw)[R]) const {
+        static_assert(UNI, "load_pol needs a workgroup-uniform tile base");
         const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(L.base, 0, 0x7FFFFFFF, 0x00020000);
 #pragma unroll
         for (int k = 0; k < R; ++k)
             raw[k] = __builtin_bit_cast(uint64_t, __builtin_amdgcn_raw_buffer_load_b64(
-                                                      rs, (int)(jidx(L, Gm::g_of(r_load, tau, k)) * 8u), 0, kSc1));
+                                                      rs, (int)(jidx(L, Gm::g_of(r_load, tau, k)) * 8u), 0, CPOL));
     }
+    __device__ __forceinline__ void load_l2(const TileLoc& L, uint64_t (&raw)[R]) const { load_pol<16>(L, raw); }
 
     __device__ __forceinline__ void compute_store(const TileLoc& L, const uint64_t (&raw)[R], uint64_t* lds) const {
         uint64_t* my_lds = lds + (size_t)gl * GS;
@@ -300,12 +328,25 @@ struct NttPass {
         if constexpr (!INV && !COLS && (NR > 1 || BREV))
             exchange(std::integral_constant<int, NR - 1>{}, std::integral_constant<int, 0>{}, BREV);
         if (L.active) {
+            if constexpr (UNI && kCpolSt != 0) {
+                const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(L.base, 0, 0x7FFFFFFF, 0x00020000);
 #pragma unroll
-            for (int k = 0; k < R; ++k) {
-                const uint32_t g = Gm::g_of(r_store, tau_, k);
-                T y = x[k];
-                if constexpr (TWIST && INV) y = ar.mulmod(y, a.twist.get(twoff + jidx(L, g)));
-                L.base[jidx(L, g)] = OUT_RAW ? A::to_raw(ar.reduce(y)) : ar.canon(y);
+                for (int k = 0; k < R; ++k) {
+                    const uint32_t g = Gm::g_of(r_store, tau_, k);
+                    T y = x[k];
+                    if constexpr (TWIST && INV) y = ar.mulmod(y, a.twist.get(twoff + jidx(L, g)));
+                    const uint64_t o = OUT_RAW ? A::to_raw(ar.reduce(y)) : ar.canon(y);
+                    __builtin_amdgcn_raw_buffer_store_b64(__builtin_bit_cast(__attribute__((ext_vector_type(2))) unsigned, o),
+                                                          rs, (int)(jidx(L, g) * 8u), 0, kCpolSt);
+                }
+            } else {
+#pragma unroll
+                for (int k = 0; k < R; ++k) {
+                    const uint32_t g = Gm::g_of(r_store, tau_, k);
+                    T y = x[k];
+                    if constexpr (TWIST && INV) y = ar.mulmod(y, a.twist.get(twoff + jidx(L, g)));
+                    L.base[jidx(L, g)] = OUT_RAW ? A::to_raw(ar.reduce(y)) : ar.canon(y);
+                }
             }
         }
     }

@@ -168,9 +168,28 @@ static int fused(const NttJob<TS>& j, hipStream_t st) {
     const int per_cu = (j.wg_per_cu > 0 && j.wg_per_cu < 16) ? std::min(j.wg_per_cu, occ) : occ;
     const uint32_t grid = (uint32_t)std::max(8, per_cu * j.num_cus);
     mfhe_ctx* c = j.ctx;
+    if (c->xcc_nq == 0) {
+        // census (once per context): which XCC ids the dispatcher uses; queue q <-> the q-th id found
+        uint32_t* dm = nullptr;
+        uint32_t mask = 0;
+        MFHE_HIP(hipMalloc(&dm, sizeof(uint32_t)));
+        hipError_t he = hipMemsetAsync(dm, 0, sizeof(uint32_t), st);
+        if (he == hipSuccess) {
+            hipLaunchKernelGGL(xcc_census_kernel, dim3(4 * j.num_cus), dim3(64), 0, st, dm);
+            he = hipGetLastError();
+        }
+        if (he == hipSuccess) he = hipMemcpyAsync(&mask, dm, sizeof(uint32_t), hipMemcpyDeviceToHost, st);
+        if (he == hipSuccess) he = hipStreamSynchronize(st);
+        (void)hipFree(dm);
+        if (he != hipSuccess) return hip_error(he, "XCC census");
+        int nq = 0;
+        for (int x = 0; x < kFusedXcc; ++x) c->xcc_qmap[x] = (mask >> x) & 1 ? (uint8_t)nq++ : 0xFF;
+        c->xcc_nq = nq > 0 ? nq : 1;
+    }
+    const uint32_t nq = (uint32_t)c->xcc_nq;
     const uint32_t lag = (uint32_t)c->ntt_fused_lag;
-    const uint64_t cap = npl + lag + 2 + grid / K + 16;
-    const size_t need = sizeof(FusedSync) + (size_t)kFusedXcc * cap * (sizeof(uint64_t) + sizeof(uint32_t));
+    const uint64_t cap = (npl + nq - 1) / nq + 1;
+    const size_t need = sizeof(FusedSync) + (size_t)kFusedXcc * cap * sizeof(uint32_t);
     if (c->fused_bytes < need) {
         if (c->fused_buf) MFHE_HIP(hipFree(c->fused_buf));
         c->fused_buf = nullptr;
@@ -197,12 +216,13 @@ static int fused(const NttJob<TS>& j, hipStream_t st) {
         a.nblocks = (uint32_t)(npl * K);
     }
     f.sync = (FusedSync*)c->fused_buf;
-    f.map = (uint64_t*)((char*)c->fused_buf + sizeof(FusedSync));
-    f.arr = (uint32_t*)(f.map + (size_t)kFusedXcc * cap);
+    f.arr = (uint32_t*)((char*)c->fused_buf + sizeof(FusedSync));
     f.cap = (uint32_t)cap;
     f.K = K;
     f.npl = (uint32_t)npl;
     f.lag = lag;
+    f.nq = nq;
+    for (int x = 0; x < kFusedXcc; ++x) f.qmap[x] = c->xcc_qmap[x];
     hipLaunchKernelGGL(kern, dim3(grid), dim3(P1::NT), lds, st, f);
     MFHE_CHECK_LAUNCH("ntt_fused_kernel launch");
     return MFHE_OK;

@@ -29,8 +29,10 @@ def main():
         import os
         mode = int(os.environ.get("FUSED_MODE", "1"))
         ctx.set_option(OPT_FUSED, mode)
-        for wg in (1, 2, 3, 4):
-            for lag in ((1, 2, 3, 4, 6, 8) if mode == 1 else (1,)):
+        wgs = [int(x) for x in os.environ.get("FUSED_WGS", "1,2,3,4").split(",")]
+        lags = [int(x) for x in os.environ.get("FUSED_LAGS", "1,2,3,4,6,8").split(",")]
+        for wg in wgs:
+            for lag in (lags if mode == 1 else (1,)):
                 ctx.set_option(OPT_WG, wg)
                 ctx.set_option(OPT_LAG, lag)
                 ctx.ntt_fwd(d, batch=batch)
@@ -40,7 +42,7 @@ def main():
                 f = t_call(lambda: ctx.ntt_fwd(d, batch=batch))
                 i = t_call(lambda: ctx.ntt_inv(d, batch=batch))
                 ntts = batch * L
-                print(json.dumps({"logN": log_n, "L": L, "batch": batch, "mode": mode, "wg": wg, "lag": lag, "fwd_ms": round(f, 4),
+                print(json.dumps({"lib": os.path.basename(os.environ.get("MFHE_LIB", "libmfhe.so")), "logN": log_n, "L": L, "batch": batch, "mode": mode, "wg": wg, "lag": lag, "fwd_ms": round(f, 4),
                                   "fwd_NTT_s": round(ntts / f * 1e3), "inv_NTT_s": round(ntts / i * 1e3),
                                   "ok": ok}), flush=True)
 
