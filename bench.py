@@ -250,32 +250,126 @@ def trace_line(reps=10):
 
 
 def cpu_baseline(log_n, moduli, seconds):
-    """Reference CPU path restated (oracle, Harvey/Shoup phantom NTT, OpenMP over polys)."""
+    """The reference's CPU path restated (oracle/, test infrastructure; the reference itself has no runnable
+    CPU path), timed on this box's host cores on bounded samples of each workload:
+      * phantom forward NTT (Harvey/Shoup, fnwt_1d semantics) at the headline shape, all cores and 1 core;
+      * encode+CRT ops (RNS decompose batched_encoder.cu:125-152 + wide CRT compose encoder.cu:191-230 +
+        big -> f64 HE.cu:1007-1027) on the same shape, all cores and 1 core;
+      * the reference's own GL NTT (ntt_core.cu:462-481) at its geometry (n = 64, L = 11, 512 x 64 polys);
+      * the C1 (N = 2^12, L = 1, single poly) and C2 (N = 2^14, L = 4, batch 256) forward NTT.
+    `cores` = OpenMP threads used for the all-core figures; nproc and the affinity mask are printed too (on
+    the GPU box nproc counts the whole machine, the process may be confined to fewer)."""
     import numpy as np
     sys.path.insert(0, str(ROOT / "tests"))
     import oracle
-    N = 1 << log_n
-    L = len(moduli)
-    threads = int(os.environ.get("OMP_NUM_THREADS", os.cpu_count() or 1))
+    aff = len(os.sched_getaffinity(0))
+    threads = int(os.environ.get("OMP_NUM_THREADS", aff))
+    N, L = 1 << log_n, len(moduli)
+    per = max(0.5, seconds / 8)          # seconds per measured figure
     rng = np.random.default_rng(0)
-    q = np.array(moduli, np.uint64)[None, :, None]
-    data = (rng.integers(0, 2 ** 63, (1, L, N), dtype=np.uint64) % q).ravel()
-    probe = np.tile(data, 8)
-    oracle.phantom_fwd(probe, L, log_n, moduli)          # warm (tables, threads)
-    t0 = time.perf_counter()
-    oracle.phantom_fwd(probe, L, log_n, moduli)
-    one = max((time.perf_counter() - t0) / 8, 1e-5)
-    batch = max(8, min(4096, int(1.0 / one)))      # ~1 s per call, repeated until `seconds` have passed
-    data = np.tile(data, batch)
-    done, dt = 0, 0.0
-    while dt < seconds:
-        t0 = time.perf_counter()
-        oracle.phantom_fwd(data, L, log_n, moduli)
-        dt += time.perf_counter() - t0
-        done += batch
-    return {"value": done * L / dt, "unit": "NTT/s", "cores": threads, "kind": "port",
-            "sample": f"{done}x{L} forward NTTs N=2^{log_n} (oracle phantom Harvey NTT, OpenMP {threads} threads, "
-                      f"{dt:.1f} s)"}
+
+    def rate(fn, units):
+        fn()                               # warm (tables, thread pool)
+        done, dt = 0, 0.0
+        while dt < per:
+            t0 = time.perf_counter()
+            fn()
+            dt += time.perf_counter() - t0
+            done += units
+        return done / dt
+
+    def residues(b, L_, n, mods):
+        q = np.array(mods, np.uint64)[None, :, None]
+        return (rng.integers(0, 2 ** 63, (b, L_, n), dtype=np.uint64) % q).ravel()
+
+    m64 = np.array(moduli, np.uint64)
+    b = 16
+    x = residues(b, L, N, moduli)
+    ntt_all = rate(lambda: oracle.L.orc_phantom_fwd(oracle.P(x), b, L, log_n, oracle.P(m64)), b * L)
+    x1 = x[: 2 * L * N].copy()
+    ntt_1 = rate(lambda: oracle.L.orc_phantom_fwd_1t(oracle.P(x1), 2, L, log_n, oracle.P(m64)), 2 * L)
+
+    # encode+CRT: one op = one real poly of N coefficients decomposed to L residues and composed back to f64
+    W = oracle.crt_words(moduli)
+    delta = 2.0 ** 35
+
+    def enc_crt(npoly, one):
+        z = rng.random(npoly * N) * 2 - 1
+        r = np.zeros(npoly * L * N, np.uint64)
+        mag = np.zeros(npoly * N * W, np.uint64)
+        neg = np.zeros(npoly * N, np.uint8)
+        out = np.zeros(npoly * N, np.float64)
+        dec = oracle.L.orc_rns_decompose_1t if one else oracle.L.orc_rns_decompose
+        com = oracle.L.orc_crt_compose_1t if one else oracle.L.orc_crt_compose
+
+        def f():
+            dec(oracle.P(z), 1, npoly, N, L, oracle.P(m64), delta, oracle.P(r))
+            com(oracle.P(r), npoly, L, N, oracle.P(m64), W, oracle.P(mag), oracle.P(neg))
+            oracle.L.orc_big_to_f64(oracle.P(mag), oracle.P(neg), npoly * N, W, delta, oracle.P(out), 1)
+        return rate(f, npoly)
+    crt_all, crt_1 = enc_crt(32, False), enc_crt(2, True)
+
+    # reference GL NTT at the reference geometry: n = 64, the 11 reference moduli, 512 x 64 polys
+    import mfhe
+    rm = mfhe.RNS_MODULI
+    g = residues(512 * 64, 11, 64, rm)
+    gl = rate(lambda: oracle.gl_fwd(g, 11, 64, rm), 512 * 64 * 11)
+    # C1 / C2 shapes
+    m12 = oracle.gen_primes(50, 1 << 14, 1)
+    c1 = residues(1, 1, 1 << 12, m12)
+    c1r = rate(lambda: oracle.phantom_fwd(c1, 1, 12, m12), 1)
+    m14 = oracle.gen_primes(50, 1 << 16, 4)
+    c2 = residues(256, 4, 1 << 14, m14)
+    c2r = rate(lambda: oracle.phantom_fwd(c2, 4, 14, m14), 256 * 4)
+    return {"value": ntt_all, "unit": "NTT/s", "cores": threads, "kind": "port",
+            "nproc": os.cpu_count(), "affinity_cores": aff,
+            "sample": f"forward NTT N=2^{log_n} x L={L} (oracle phantom Harvey NTT, OpenMP {threads} threads), "
+                      f"~{per:.1f} s per figure; the headline workload is 1024 polys x {L} limbs, sampled at "
+                      f"{b} polys per call",
+            "one_core_NTT_per_s": ntt_1,
+            "encode_crt_ops_per_s": {"all_cores": crt_all, "one_core": crt_1,
+                                     "op": f"decompose + wide CRT compose + f64 of one N=2^{log_n} poly, L={L}, W={W}"},
+            "gl_ntt_reference_geometry_NTT_per_s": gl,
+            "C1_fwd_NTT_per_s": c1r, "C2_fwd_NTT_per_s": c2r}
+
+
+def u64_line(reps=10):
+    """C3 forward NTT on the 64-bit integer path (ArithU64, Harvey/Shoup): 60-bit primes, which the FP64 path
+    cannot take (q < 2^50), and the headline's 50-bit primes forced onto U64 for comparison."""
+    import torch
+    import mfhe
+    log_n, L, batch = 16, 8, 1024
+    N = 1 << log_n
+    res = {}
+    for name, bits, arith in (("60-bit primes (auto -> u64)", 60, 0), ("50-bit primes, u64 forced", 50, mfhe.ARITH_U64)):
+        moduli = gen_moduli(bits, 1 << (log_n + 2), L)
+        ctx = mfhe.Context(moduli, log_n, mfhe.CONV_PHANTOM)
+        if arith:
+            ctx.set_arith(arith)
+        d = torch.empty(batch * L * N, dtype=torch.int64, device="cuda")
+        qt = torch.tensor(moduli, dtype=torch.int64, device="cuda").repeat_interleave(N).repeat(batch)
+        d.random_(0, 2 ** 62).remainder_(qt)
+        del qt
+        out = {}
+        for kind, fn in (("fwd", ctx.ntt_fwd), ("inv", ctx.ntt_inv)):
+            fn(d, batch=batch)
+            torch.cuda.synchronize()
+            e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            e0.record()
+            for _ in range(reps):
+                fn(d, batch=batch)
+            e1.record()
+            torch.cuda.synchronize()
+            r = batch * L / (e0.elapsed_time(e1) / reps * 1e-3)
+            out[f"{kind}_NTT_per_s"] = round(r)
+            out[f"{kind}_alg_GBps"] = round(16.0 * N * r / 1e9, 1)
+        out["frac_fwd"] = round(out["fwd_alg_GBps"] / HBM_PEAK_GBS, 4)
+        out["arith"] = "u64" if ctx.info().arith == mfhe.ARITH_U64 else "f64"
+        out["max_modulus_bits"] = max(moduli).bit_length()
+        res[name] = out
+        del d
+        ctx.close()
+    return res
 
 
 def main():
@@ -379,6 +473,13 @@ def main():
         shard = full.view(rb, L, N)[:, s0:s0 + lg, :].contiguous().view(-1)
         del full, zr
         rout = torch.empty(rb // world * N, dtype=torch.float64, device=dev)
+        # multi-GPU: the recombine is the native RCCL call (mfhe_crt_recombine_sharded) on a communicator
+        # owned by libmfhe, receive buffers reserved here, outside the timed steps
+        comm = None
+        if world > 1 and backend == "nccl":
+            comm = mfhe.Comm.create()
+            for mode in ("allgather", "alltoall"):
+                ctx.crt_recombine_reserve(comm, mode, rb, N)
         rc = {}
         nrep = max(1, args.steps // 4)
         modes = ("allgather", "alltoall") if world > 1 else ("local",)
@@ -389,7 +490,7 @@ def main():
                 if mode == "local":
                     ctx.crt_compose_f64(shard, rout, rb, N, stream=stream)
                 else:
-                    mdist.crt_recombine(ctx, shard, rb, N, mode, out=rout, stream=stream)
+                    mdist.crt_recombine(ctx, shard, rb, N, mode, out=rout, stream=stream, comm=comm)
             w_r, _ = timed(step, nrep, 1)
             rc[mode] = w_r / nrep
 
@@ -397,7 +498,12 @@ def main():
             ctx.ntt_fwd(shard, batch=rb, start_limb=s0, nlimbs=lg, stream=stream)
             ctx.ntt_inv(shard, batch=rb, start_limb=s0, nlimbs=lg, stream=stream)
         w_n, _ = timed(ntt_rt, nrep, 1)
+        if comm is not None:
+            comm.close()
         res["recombine"] = {"batch": rb, "limbs_per_gpu": lg, "ntt_roundtrip_only_ms": w_n / nrep * 1e3,
+                            "exchange": ("none (1 GPU: local compose)" if world == 1 else "native RCCL (mfhe_crt_recombine_sharded)")
+                                        if comm is not None or world == 1
+                                        else "torch.distributed " + backend,
                             **{f"{m}_ms": t * 1e3 for m, t in rc.items()},
                             **{f"{m}_polys_per_s": rb / t for m, t in rc.items()}}
 
@@ -453,6 +559,7 @@ def main():
             out["reference_geometry_pipeline"] = pipeline_line()
             out["other_ntt_configs"] = other_configs_line()
             out["trace_gemm_reference_geometry"] = trace_line()
+            out["u64_path_c3_forward_ntt"] = u64_line()
         if world == 1 and not args.no_cpu_baseline and args.only == "all":
             try:
                 out["cpu_baseline"] = cpu_baseline(log_n, moduli, args.cpu_seconds)

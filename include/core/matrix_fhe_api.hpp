@@ -18,11 +18,13 @@
 #include <hip/hip_runtime.h>
 
 #include <cstdint>
+#include <array>
 #include <stdexcept>
 #include <string>
 
 class DNTTTable;  // phantom surface, include/phantom/phantom_api.hpp
 struct mfhe_ctx;
+struct mfhe_comm;
 
 namespace matrix_fhe {
 
@@ -169,6 +171,33 @@ void trace_gemm_batched(const uint64_t* A_real, const uint64_t* A_imag, const ui
                         int batch_size);
 void rescale_by_delta_batched(uint64_t* C_real, uint64_t* C_imag, int n, int rns_limbs, int batch_size,
                               uint64_t inv0, uint64_t inv1, uint64_t inv2);
+
+// ---- multi-GPU residue sharding (extension: the reference is single-GPU) ----
+// Decode's per-lane compose loop (HE.cu:1653-1668 -> crt_compose_centerlift_big) over limbs sharded across
+// GPUs: rank g of G holds limbs [g*limbs/G, (g+1)*limbs/G) of every lane as [lanes][limbs/G][n2] (the
+// matrix-major shard of the W-INTT output).  One RCCL communicator per process/GPU.
+class ResidueComm {
+   public:
+    static constexpr int kIdBytes = 128;
+    // rank 0 draws the id; the caller hands the same bytes to every rank (MPI, a file, a socket...)
+    static std::array<uint8_t, kIdBytes> unique_id();
+    ResidueComm(const std::array<uint8_t, kIdBytes>& id, int nranks, int rank);   // collective
+    ~ResidueComm();
+    ResidueComm(const ResidueComm&) = delete;
+    ResidueComm& operator=(const ResidueComm&) = delete;
+    int size() const { return nranks_; }
+    int rank() const { return rank_; }
+    ::mfhe_comm* handle() const { return comm_; }
+
+   private:
+    ::mfhe_comm* comm_ = nullptr;
+    int nranks_ = 1, rank_ = 0;
+};
+// Exchange (all-gather, or all-to-all when `alltoall`) + compose of this rank's lane slice
+// [g*lanes/G, (g+1)*lanes/G) to centred value / SCALING_FACTOR: d_out [lanes/G][n2] f64, bit-identical to the
+// single-GPU compose of the unsharded residues.  Moduli RNS_MODULI[0..limbs).
+void crt_recombine_sharded(ResidueComm& comm, const uint64_t* d_shard, double* d_out, int n2, int limbs, int lanes,
+                           bool alltoall = false, hipStream_t stream = 0);
 
 // The C-ABI context (include/mfhe.h) behind this API for a given (n, limbs): moduli RNS_MODULI[0..limbs),
 // delta = SCALING_FACTOR, phantom + GL (+ W-CRT when with_wcrt) tables.  Built once, cached.

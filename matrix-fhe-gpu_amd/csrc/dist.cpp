@@ -1,0 +1,224 @@
+// dist.cpp -- multi-GPU residue sharding over RCCL (xGMI): the C-ABI exchange + sharded wide-CRT recombine.
+//
+// NTT, RNS decompose and W-CRT are independent per RNS limb, so rank g of G owns limbs
+// [g*L/G, (g+1)*L/G) of every polynomial and transforms them with no communication.  The wide CRT compose
+// needs all L residues of a coefficient: that is the one exchange step.  It replaces the reference's
+// single-GPU per-lane compose loop (src/core/HE.cu:1653-1668 -> crt_compose_centerlift_big,
+// src/core/encoder.cu:191-245); the reference itself has no multi-GPU code.
+//
+// RCCL is loaded with dlopen on first use (librccl.so.1 from ROCm), so libmfhe.so itself carries no
+// link-time RCCL dependency and loads on hosts without it; calls then return MFHE_EUNSUPPORTED.
+//
+// Exchanges (each rank's slice of the batch is [g*B/G, (g+1)*B/G)):
+//   all-gather : every rank receives every shard, [G][B][L/G][n]; composes its slice in place.
+//   all-to-all : chunk r of a rank's shard (the polys of rank r's slice) goes to rank r, so each rank
+//                receives only the missing limbs of its own slice, [G][B/G][L/G][n].
+// Both feed mfhe_crt_compose_f64_sharded, which reads the shards in place (no transpose).  The receive
+// buffer is owned by the communicator and grown by mfhe_crt_recombine_reserve, outside timed code.
+#include <dlfcn.h>
+
+#include <cstring>
+#include <mutex>
+#include <type_traits>
+#include <rccl/rccl.h>
+
+#include "mfhe_ctx.hpp"
+
+namespace {
+
+struct Rccl {
+    bool ok = false;
+    ncclResult_t (*GetUniqueId)(ncclUniqueId*) = nullptr;
+    ncclResult_t (*CommInitRank)(ncclComm_t*, int, ncclUniqueId, int) = nullptr;
+    ncclResult_t (*CommDestroy)(ncclComm_t) = nullptr;
+    ncclResult_t (*CommCount)(const ncclComm_t, int*) = nullptr;
+    ncclResult_t (*CommUserRank)(const ncclComm_t, int*) = nullptr;
+    ncclResult_t (*AllGather)(const void*, void*, size_t, ncclDataType_t, ncclComm_t, hipStream_t) = nullptr;
+    ncclResult_t (*AllToAll)(const void*, void*, size_t, ncclDataType_t, ncclComm_t, hipStream_t) = nullptr;
+    const char* (*GetErrorString)(ncclResult_t) = nullptr;
+};
+
+const Rccl& rccl() {
+    static Rccl r;
+    static std::once_flag once;
+    std::call_once(once, [] {
+        void* h = dlopen("librccl.so.1", RTLD_NOW | RTLD_GLOBAL);
+        if (!h) h = dlopen("librccl.so", RTLD_NOW | RTLD_GLOBAL);
+        if (!h) return;
+        auto sym = [&](auto& fp, const char* name) {
+            fp = reinterpret_cast<std::remove_reference_t<decltype(fp)>>(dlsym(h, name));
+            return fp != nullptr;
+        };
+        r.ok = sym(r.GetUniqueId, "ncclGetUniqueId") && sym(r.CommInitRank, "ncclCommInitRank") &&
+               sym(r.CommDestroy, "ncclCommDestroy") && sym(r.CommCount, "ncclCommCount") &&
+               sym(r.CommUserRank, "ncclCommUserRank") && sym(r.AllGather, "ncclAllGather") &&
+               sym(r.AllToAll, "ncclAllToAll") && sym(r.GetErrorString, "ncclGetErrorString");
+    });
+    return r;
+}
+
+int nccl_error(ncclResult_t e, const char* what) {
+    const Rccl& r = rccl();
+    return mfhe::set_error(MFHE_EHIP, std::string(what) + ": " + (r.GetErrorString ? r.GetErrorString(e) : "RCCL error"));
+}
+
+int need_rccl() {
+    if (!rccl().ok) return mfhe::set_error(MFHE_EUNSUPPORTED, "RCCL (librccl.so.1) could not be loaded");
+    return MFHE_OK;
+}
+
+}  // namespace
+
+struct mfhe_comm {
+    ncclComm_t comm = nullptr;
+    bool owned = false;
+    int nranks = 1, rank = 0, device = 0;
+    void* recv = nullptr;   // receive buffer of the recombine exchange
+    size_t recv_bytes = 0;
+};
+
+using mfhe::set_error;
+
+extern "C" int mfhe_comm_unique_id(uint8_t* id) {
+    if (!id) return set_error(MFHE_EINVAL, "null id");
+    if (int rc = need_rccl()) return rc;
+    ncclUniqueId u;
+    ncclResult_t e = rccl().GetUniqueId(&u);
+    if (e != ncclSuccess) return nccl_error(e, "ncclGetUniqueId");
+    std::memcpy(id, u.internal, MFHE_COMM_ID_BYTES);
+    return MFHE_OK;
+}
+
+extern "C" int mfhe_comm_init(const uint8_t* id, int nranks, int rank, mfhe_comm** out) {
+    if (!id || !out || nranks < 1 || rank < 0 || rank >= nranks) return set_error(MFHE_EINVAL, "mfhe_comm_init: bad argument");
+    *out = nullptr;
+    if (int rc = need_rccl()) return rc;
+    ncclUniqueId u;
+    std::memcpy(u.internal, id, MFHE_COMM_ID_BYTES);
+    mfhe_comm* c = new mfhe_comm();
+    hipError_t he = hipGetDevice(&c->device);
+    if (he != hipSuccess) {
+        delete c;
+        return mfhe::hip_error(he, "hipGetDevice");
+    }
+    ncclResult_t e = rccl().CommInitRank(&c->comm, nranks, u, rank);
+    if (e != ncclSuccess) {
+        delete c;
+        return nccl_error(e, "ncclCommInitRank");
+    }
+    c->owned = true;
+    c->nranks = nranks;
+    c->rank = rank;
+    *out = c;
+    return MFHE_OK;
+}
+
+extern "C" int mfhe_comm_wrap(void* nccl_comm, mfhe_comm** out) {
+    if (!nccl_comm || !out) return set_error(MFHE_EINVAL, "mfhe_comm_wrap: null argument");
+    *out = nullptr;
+    if (int rc = need_rccl()) return rc;
+    mfhe_comm* c = new mfhe_comm();
+    c->comm = (ncclComm_t)nccl_comm;
+    ncclResult_t e = rccl().CommCount(c->comm, &c->nranks);
+    if (e == ncclSuccess) e = rccl().CommUserRank(c->comm, &c->rank);
+    if (e != ncclSuccess) {
+        delete c;
+        return nccl_error(e, "ncclCommCount/UserRank");
+    }
+    (void)hipGetDevice(&c->device);
+    *out = c;
+    return MFHE_OK;
+}
+
+extern "C" int mfhe_comm_destroy(mfhe_comm* c) {
+    if (!c) return MFHE_OK;
+    int rc = MFHE_OK;
+    if (c->recv) {
+        hipError_t he = hipFree(c->recv);
+        if (he != hipSuccess) rc = mfhe::hip_error(he, "hipFree");
+    }
+    if (c->owned && c->comm) {
+        ncclResult_t e = rccl().CommDestroy(c->comm);
+        if (e != ncclSuccess && !rc) rc = nccl_error(e, "ncclCommDestroy");
+    }
+    delete c;
+    return rc;
+}
+
+extern "C" int mfhe_comm_info(const mfhe_comm* c, int* nranks, int* rank) {
+    if (!c) return set_error(MFHE_EINVAL, "null comm");
+    if (nranks) *nranks = c->nranks;
+    if (rank) *rank = c->rank;
+    return MFHE_OK;
+}
+
+extern "C" int mfhe_allgather_limbs(mfhe_comm* c, const uint64_t* d_shard, size_t count, uint64_t* d_recv,
+                                    mfhe_stream_t s) {
+    if (!c) return set_error(MFHE_EINVAL, "null comm");
+    if (count == 0) return MFHE_OK;
+    if (!d_shard || !d_recv) return set_error(MFHE_EINVAL, "mfhe_allgather_limbs: null buffer");
+    ncclResult_t e = rccl().AllGather(d_shard, d_recv, count, ncclUint64, c->comm, (hipStream_t)s);
+    return e == ncclSuccess ? MFHE_OK : nccl_error(e, "ncclAllGather");
+}
+
+namespace {
+
+// receive-buffer words of one recombine exchange
+int xchg_shape(const mfhe_ctx* ctx, const mfhe_comm* c, int mode, size_t npoly, size_t ncoeff, size_t* words) {
+    if (!ctx || !c) return set_error(MFHE_EINVAL, "null ctx / comm");
+    const int G = c->nranks;
+    if (ctx->L % G) return set_error(MFHE_EINVAL, "recombine: the communicator size must divide L");
+    if (npoly % (size_t)G) return set_error(MFHE_EINVAL, "recombine: the communicator size must divide npoly");
+    if (mode != MFHE_XCHG_ALLGATHER && mode != MFHE_XCHG_ALLTOALL) return set_error(MFHE_EINVAL, "recombine: bad mode");
+    const size_t shard = npoly * (size_t)(ctx->L / G) * ncoeff;   // this rank's [npoly][L/G][ncoeff]
+    *words = mode == MFHE_XCHG_ALLGATHER ? shard * G : shard;     // all-to-all: G chunks of shard / G
+    return MFHE_OK;
+}
+
+int grow(mfhe_comm* c, size_t bytes) {
+    if (c->recv_bytes >= bytes) return MFHE_OK;
+    if (c->recv) MFHE_HIP(hipFree(c->recv));
+    c->recv = nullptr;
+    c->recv_bytes = 0;
+    hipError_t he = hipMalloc(&c->recv, bytes);
+    if (he != hipSuccess) return set_error(MFHE_ENOMEM, "recombine receive buffer: hipMalloc failed");
+    c->recv_bytes = bytes;
+    return MFHE_OK;
+}
+
+}  // namespace
+
+extern "C" int mfhe_crt_recombine_reserve(mfhe_ctx* ctx, mfhe_comm* c, int mode, size_t npoly, size_t ncoeff) {
+    size_t words = 0;
+    if (int rc = xchg_shape(ctx, c, mode, npoly, ncoeff, &words)) return rc;
+    return grow(c, words * sizeof(uint64_t));
+}
+
+extern "C" int mfhe_crt_recombine_sharded(mfhe_ctx* ctx, mfhe_comm* c, int mode, const uint64_t* d_shard,
+                                          size_t npoly, size_t ncoeff, double* d_out, size_t out_stride,
+                                          mfhe_stream_t s) {
+    size_t words = 0;
+    if (int rc = xchg_shape(ctx, c, mode, npoly, ncoeff, &words)) return rc;
+    if (npoly == 0 || ncoeff == 0) return MFHE_OK;
+    if (!d_shard || !d_out || out_stride == 0) return set_error(MFHE_EINVAL, "recombine: bad pointer / stride");
+    if (int rc = need_rccl()) return rc;
+    if (int rc = grow(c, words * sizeof(uint64_t))) return rc;
+    const int G = c->nranks;
+    const size_t bs = npoly / G, lg = (size_t)(ctx->L / G);
+    const size_t shard = npoly * lg * ncoeff;
+    uint64_t* recv = static_cast<uint64_t*>(c->recv);
+    const hipStream_t st = (hipStream_t)s;
+    ncclResult_t e;
+    size_t off, stride;
+    if (mode == MFHE_XCHG_ALLGATHER) {
+        e = rccl().AllGather(d_shard, recv, shard, ncclUint64, c->comm, st);
+        off = (size_t)c->rank * bs * lg * ncoeff;   // my slice inside every gathered shard
+        stride = shard;
+    } else {
+        e = rccl().AllToAll(d_shard, recv, bs * lg * ncoeff, ncclUint64, c->comm, st);
+        off = 0;
+        stride = bs * lg * ncoeff;
+    }
+    if (e != ncclSuccess) return nccl_error(e, mode == MFHE_XCHG_ALLGATHER ? "ncclAllGather" : "ncclAllToAll");
+    return mfhe_crt_compose_f64_sharded(ctx, recv + off, G, stride, bs, ncoeff, d_out, out_stride, s);
+}

@@ -26,6 +26,8 @@ ARITH_AUTO, ARITH_F64, ARITH_U64 = 0, 1, 2
 OPT_NTT_CHUNK_BYTES, OPT_NTT_PLAN, OPT_CRT_WORDS, OPT_NTT_WG_PER_CU, OPT_NTT_PREFETCH = 1, 2, 3, 4, 5
 OPT_NTT_FUSED, OPT_NTT_FUSED_LAG, OPT_NTT_FUSED_ERRORS, OPT_WCRT_MFMA = 6, 7, 8, 9
 OPT_CGEMM_MFMA, OPT_HE_FUSED, OPT_TRACE_SPLIT = 10, 11, 12
+XCHG_ALLGATHER, XCHG_ALLTOALL = 0, 1
+COMM_ID_BYTES = 128
 
 #: reference parameters (include/core/config.h:7-52)
 RNS_MODULI = [
@@ -114,6 +116,14 @@ _sig("mfhe_encrypt", [_vp, _vp, _vp, _vp, _vp])
 _sig("mfhe_encrypt_pair", [_vp, _vp, _vp, _vp, _vp, _vp, _vp])
 _sig("mfhe_decrypt_to_eval", [_vp, _vp, _vp, _vp, _vp])
 _sig("mfhe_decrypt_and_decode", [_vp, _vp, _vp, _vp, _vp, _vp])
+_sig("mfhe_comm_unique_id", [_vp])
+_sig("mfhe_comm_init", [_vp, ctypes.c_int, ctypes.c_int, ctypes.POINTER(_vp)])
+_sig("mfhe_comm_wrap", [_vp, ctypes.POINTER(_vp)])
+_sig("mfhe_comm_destroy", [_vp])
+_sig("mfhe_comm_info", [_vp, ctypes.POINTER(ctypes.c_int), ctypes.POINTER(ctypes.c_int)])
+_sig("mfhe_allgather_limbs", [_vp, _vp, _sz, _vp, _vp])
+_sig("mfhe_crt_recombine_sharded", [_vp, _vp, ctypes.c_int, _vp, _sz, _sz, _vp, _sz, _vp])
+_sig("mfhe_crt_recombine_reserve", [_vp, _vp, ctypes.c_int, _sz, _sz])
 _sig("mfhe_last_error", [], ctypes.c_char_p)
 _sig("mfhe_version", [], ctypes.c_char_p)
 
@@ -131,6 +141,68 @@ def declared_symbols(header: Path = None) -> list[str]:
 def check(rc: int, what: str = "") -> None:
     if rc != OK:
         raise MfheError(rc, f"{what}: {lib.mfhe_last_error().decode()}")
+
+
+_XCHG = {"allgather": XCHG_ALLGATHER, "alltoall": XCHG_ALLTOALL}
+
+
+def _need(t, words, what):
+    """Host-side size check before a raw pointer crosses the C ABI (an undersized tensor would otherwise be
+    an out-of-bounds device access)."""
+    if t.numel() * t.element_size() < 8 * words:
+        raise ValueError(f"{what}: {t.numel()} elements of {t.element_size()} B < {words} words needed")
+
+
+class Comm:
+    """An RCCL communicator owned by libmfhe (include/mfhe.h mfhe_comm_*): one per process/GPU.
+
+    `Comm.create(rank, world, group)` makes rank 0 draw the unique id and broadcasts it over an existing
+    torch.distributed process group (any backend) -- the side channel only; the data path is RCCL."""
+
+    def __init__(self, handle, size, rank):
+        self._h, self.size, self.rank = handle, size, rank
+
+    @classmethod
+    def from_id(cls, uid: bytes, world: int, rank: int) -> "Comm":
+        buf = (ctypes.c_uint8 * COMM_ID_BYTES).from_buffer_copy(uid)
+        h = _vp()
+        check(lib.mfhe_comm_init(ctypes.addressof(buf), world, rank, ctypes.byref(h)), "comm_init")
+        return cls(h, world, rank)
+
+    @staticmethod
+    def unique_id() -> bytes:
+        buf = (ctypes.c_uint8 * COMM_ID_BYTES)()
+        check(lib.mfhe_comm_unique_id(ctypes.addressof(buf)), "comm_unique_id")
+        return bytes(buf)
+
+    @classmethod
+    def create(cls, group=None) -> "Comm":
+        import torch
+        import torch.distributed as dist
+        rank, world = dist.get_rank(group), dist.get_world_size(group)
+        uid = cls.unique_id() if rank == 0 else bytes(COMM_ID_BYTES)
+        t = torch.tensor(list(uid), dtype=torch.uint8)
+        if dist.get_backend(group) == "nccl":
+            t = t.cuda()
+        dist.broadcast(t, src=dist.get_global_rank(group, 0) if group is not None else 0, group=group)
+        return cls.from_id(bytes(t.cpu().tolist()), world, rank)
+
+    def allgather_limbs(self, shard, recv, stream=None):
+        _need(recv, shard.numel() * self.size, "recv")
+        check(lib.mfhe_allgather_limbs(self._h, _ptr(shard), shard.numel(), _ptr(recv), _stream_ptr(stream)),
+              "allgather_limbs")
+        return recv
+
+    def close(self):
+        if self._h:
+            check(lib.mfhe_comm_destroy(self._h), "comm_destroy")
+            self._h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
 
 
 def _stream_ptr(stream) -> int:
@@ -267,6 +339,22 @@ class Context:
                                                ncoeff, _ptr(out), out_stride, _stream_ptr(stream)),
               "crt_compose_f64_sharded")
         return out
+
+    def crt_recombine_sharded(self, comm: "Comm", mode, shard, npoly, ncoeff, out, out_stride=1, stream=None):
+        """RCCL exchange of this rank's [npoly][L/G][ncoeff] residue shard + compose of its polynomial slice
+        (include/mfhe.h mfhe_crt_recombine_sharded); out: npoly/G * ncoeff f64."""
+        m = _XCHG[mode] if isinstance(mode, str) else mode
+        g = comm.size
+        lg = self.info().num_limbs // g if g else 0
+        _need(shard, npoly * lg * ncoeff, "shard")
+        _need(out, (npoly // g) * ncoeff if g else 0, "out")
+        check(lib.mfhe_crt_recombine_sharded(self._h, comm._h, m, _ptr(shard), npoly, ncoeff, _ptr(out), out_stride,
+                                             _stream_ptr(stream)), "crt_recombine_sharded")
+        return out
+
+    def crt_recombine_reserve(self, comm: "Comm", mode, npoly, ncoeff):
+        m = _XCHG[mode] if isinstance(mode, str) else mode
+        check(lib.mfhe_crt_recombine_reserve(self._h, comm._h, m, npoly, ncoeff), "crt_recombine_reserve")
 
     # ---- W axis / encoder / pipelines (reference geometry, CONV_WCRT) ----
     def _call(self, name, *ptrs, stream=None):

@@ -11,8 +11,11 @@ so it is the one exchange step.  Rank g recombines the batch slice [g*B/world, (
               missing limbs of its own slice ((world-1)/world^2 of the residue set).
 
 Both hand the received buffer to mfhe_crt_compose_f64_sharded, which reads the shards in place
-(no transpose).  On GPU the process group is RCCL (backend "nccl"); the CPU tests drive the same
-exchange over gloo.
+(no transpose).  On GPU the whole step is one C-ABI call, mfhe_crt_recombine_sharded, over an RCCL
+communicator owned by libmfhe (mfhe.Comm; receive buffer preallocated by crt_recombine_reserve), so a C++
+caller of the reference API shards residues the same way.  exchange_residues restates the exchange with
+torch.distributed collectives: it is what the gloo CPU tests drive to pin the shard layout the native
+call produces (same offsets, same strides).
 """
 from __future__ import annotations
 
@@ -54,11 +57,17 @@ def exchange_residues(shard: torch.Tensor, batch: int, lg: int, ncoeff: int, mod
 
 
 def crt_recombine(ctx, shard: torch.Tensor, batch: int, ncoeff: int, mode: str = "allgather", group=None,
-                  out: torch.Tensor | None = None, stream=None) -> torch.Tensor:
+                  out: torch.Tensor | None = None, stream=None, comm=None) -> torch.Tensor:
     """Exchange residue shards and compose this rank's batch slice to f64 (centred value / delta).
 
     `ctx` is an mfhe.Context over all L moduli (its CRT tables); returns [batch/world][ncoeff] f64.
+    With `comm` (an mfhe.Comm) the exchange + compose is the native mfhe_crt_recombine_sharded (RCCL);
+    without it the exchange goes through torch.distributed on `group`.
     """
+    if comm is not None:
+        if out is None:
+            out = torch.empty(batch // comm.size * ncoeff, dtype=torch.float64, device=shard.device)
+        return ctx.crt_recombine_sharded(comm, mode, shard, batch, ncoeff, out, stream=stream)
     world = dist.get_world_size(group)
     L = ctx.info().num_limbs
     _, lg = limb_range(L, world, 0)

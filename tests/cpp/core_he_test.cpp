@@ -77,6 +77,35 @@ int main() {
         hipFree(din); hipFree(mag); hipFree(neg);
     }
 
+    // ---- sharded recombine through a 1-rank RCCL communicator == single-GPU compose (extension) ----
+    std::printf("[crt recombine, 1-rank RCCL]\n");
+    {
+        const int lanes = 4, cnt = 64;
+        std::vector<uint64_t> rns((size_t)lanes * L * cnt);
+        uint64_t s2 = 99;
+        for (int w = 0; w < lanes; ++w)
+            for (int i = 0; i < cnt; ++i) {
+                const int64_t v = (int64_t)(splitmix(s2) >> 20) - (1ll << 43);
+                for (int l = 0; l < L; ++l) {
+                    int64_t r = v % (int64_t)RNS_MODULI[l];
+                    rns[((size_t)w * L + l) * cnt + i] = (uint64_t)(r < 0 ? r + (int64_t)RNS_MODULI[l] : r);
+                }
+            }
+        uint64_t* din = h2d(rns);
+        double* out = dev_alloc<double>((size_t)lanes * cnt);
+        ResidueComm comm(ResidueComm::unique_id(), 1, 0);
+        for (int a2a = 0; a2a < 2; ++a2a) {
+            crt_recombine_sharded(comm, din, out, cnt, L, lanes, a2a != 0);
+            auto ho = d2h(out, (size_t)lanes * cnt);
+            s2 = 99;
+            for (size_t i = 0; i < ho.size(); ++i) {
+                const int64_t v = (int64_t)(splitmix(s2) >> 20) - (1ll << 43);
+                EXPECT(ho[i] == (double)v / SCALING_FACTOR, "recombine value %zu (alltoall %d)", i, a2a);
+            }
+        }
+        hipFree(din); hipFree(out);
+    }
+
     // ---- W-CRT forward / inverse exact round trip (HE.cu:437-452) ----
     std::printf("[wcrt]\n");
     const size_t words = (size_t)PHI * L * n2;

@@ -1,0 +1,93 @@
+"""Native multi-GPU recombine (include/mfhe.h mfhe_comm_* / mfhe_crt_recombine_sharded) on one GPU.
+
+A 1-rank RCCL communicator runs the real exchange code path (ncclAllGather / ncclAllToAll into the
+communicator-owned receive buffer, then the sharded compose) and must equal the unsharded
+mfhe_crt_compose_f64 bit for bit.  RCCL refuses two ranks on one GPU, so the G > 1 layout is pinned by the
+gloo tests in test_dist_cpu.py (same offsets and strides) and by the sharded-compose kernel test below,
+which feeds it G shards laid out exactly as the G-rank exchanges deliver them.
+"""
+import numpy as np
+import pytest
+
+pytestmark = pytest.mark.gpu
+
+
+def _residues(rng, npoly, moduli, ncoeff, delta):
+    """RNS residues of centred values |v| < 2^40 (the decode regime), [npoly][L][ncoeff]."""
+    v = rng.integers(-(1 << 40), 1 << 40, (npoly, ncoeff), dtype=np.int64)
+    q = np.array(moduli, dtype=object)
+    return np.stack([(v.astype(object) % int(m)).astype(np.uint64) for m in q], axis=1), v
+
+
+@pytest.mark.parametrize("mode", ["allgather", "alltoall"])
+def test_recombine_one_rank_equals_unsharded(mfhe, orc, mode):
+    import torch
+    moduli = orc.gen_primes(50, 1 << 18, 8)
+    ctx = mfhe.Context(moduli, 16)
+    npoly, ncoeff = 6, 1 << 12
+    rng = np.random.default_rng(3)
+    res, v = _residues(rng, npoly, moduli, ncoeff, ctx.info().delta)
+    d = mfhe.to_device_u64(res.ravel())
+    comm = mfhe.Comm.from_id(mfhe.Comm.unique_id(), 1, 0)
+    try:
+        ctx.crt_recombine_reserve(comm, mode, npoly, ncoeff)
+        out = torch.empty(npoly * ncoeff, dtype=torch.float64, device="cuda")
+        ctx.crt_recombine_sharded(comm, mode, d, npoly, ncoeff, out)
+        ref = torch.empty_like(out)
+        ctx.crt_compose_f64(d, ref, npoly, ncoeff)
+        torch.cuda.synchronize()
+        assert torch.equal(out, ref)
+        np.testing.assert_array_equal(out.cpu().numpy(), v.ravel().astype(np.float64) / ctx.info().delta)
+        # raw exchange: a 1-rank all-gather is a copy
+        recv = torch.empty_like(d)
+        comm.allgather_limbs(d, recv)
+        torch.cuda.synchronize()
+        assert torch.equal(recv, d)
+    finally:
+        comm.close()
+        ctx.close()
+
+
+def test_recombine_rejects_bad_shapes(mfhe, orc):
+    import torch
+    moduli = orc.gen_primes(50, 1 << 14, 3)
+    ctx = mfhe.Context(moduli, 12)
+    comm = mfhe.Comm.from_id(mfhe.Comm.unique_id(), 1, 0)
+    try:
+        d = torch.zeros(4 * 3 * 16, dtype=torch.int64, device="cuda")
+        out = torch.zeros(4 * 16, dtype=torch.float64, device="cuda")
+        with pytest.raises(mfhe.MfheError):
+            ctx.crt_recombine_sharded(comm, 7, d, 4, 16, out)
+        with pytest.raises(ValueError):   # undersized shard caught on the host
+            ctx.crt_recombine_sharded(comm, "allgather", d[:10], 4, 16, out)
+    finally:
+        comm.close()
+        ctx.close()
+
+
+@pytest.mark.parametrize("G,mode", [(2, "allgather"), (4, "allgather"), (2, "alltoall"), (4, "alltoall")])
+def test_sharded_compose_layout_of_g_rank_exchange(mfhe, orc, G, mode):
+    """What rank g composes after a G-rank exchange, built on one GPU in the exact receive layout the
+    native call uses (all-gather: [G][B][L/G][n] at offset g*B/G; all-to-all: [G][B/G][L/G][n])."""
+    import torch
+    L, B, n = 8, 8, 256
+    moduli = orc.gen_primes(50, 1 << 14, L)
+    ctx = mfhe.Context(moduli, 12)
+    rng = np.random.default_rng(G)
+    res, _ = _residues(rng, B, moduli, n, ctx.info().delta)
+    lg, bs = L // G, B // G
+    shards = [res[:, g * lg:(g + 1) * lg, :] for g in range(G)]          # rank g's [B][L/G][n]
+    ref = torch.empty(B * n, dtype=torch.float64, device="cuda")
+    ctx.crt_compose_f64(mfhe.to_device_u64(res.ravel()), ref, B, n)
+    for g in range(G):
+        if mode == "allgather":
+            recv = np.concatenate([s.ravel() for s in shards])
+            off, stride = g * bs * lg * n, B * lg * n
+        else:
+            recv = np.concatenate([s[g * bs:(g + 1) * bs].ravel() for s in shards])
+            off, stride = 0, bs * lg * n
+        out = torch.empty(bs * n, dtype=torch.float64, device="cuda")
+        ctx.crt_compose_f64_sharded(mfhe.to_device_u64(recv), out, G, stride, bs, n, src_offset=off)
+        torch.cuda.synchronize()
+        assert torch.equal(out, ref[g * bs * n:(g + 1) * bs * n])
+    ctx.close()
