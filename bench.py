@@ -43,7 +43,7 @@ def parse():
     ap.add_argument("--no-pipeline", action="store_true",
                     help="skip the reference-geometry pipeline and other-config NTT lines (N=1 only)")
     ap.add_argument("--cpu-seconds", type=float, default=10.0)
-    ap.add_argument("--only", default="all", help="all | ntt | crt | recombine (profiling)")
+    ap.add_argument("--only", default="all", help="all | ntt | crt | recombine | c4 (profiling)")
     ap.add_argument("--recombine-batch", type=int, default=256,
                     help="polys per step for the residue-shard INTT + CRT recombine line (0 = skip)")
     return ap.parse_args()
@@ -247,6 +247,62 @@ def trace_line(reps=10):
             "kernel": "split-digit product on v_mfma_f64_16x16x4 (16 MFMA per 16x16x4 complex block-step, exact)",
             "fp64_tflops": round(macs * 16 * 2 / (g_ms * 1e-3) / 1e12, 1), "fp64_peak_tflops": 78.6,
             "modmul_kernel_gemm_ms": round(m_ms, 3), "split_valu_kernel_gemm_ms": round(x_ms, 3)}
+
+
+def c4_line(world, rank, comm, barrier, reps=5):
+    """BASELINE C4: encode -> encrypt_pair -> decrypt_and_decode with wide CRT at the reference geometry (n = 64,
+    512 W-lanes), L = 16 moduli q = 1 mod 2^8 * 771, residues sharded across the ranks: rank g runs every
+    per-limb stage (W-CRT, samplers, X-NTT ring products, W-INTT) on limbs [g*16/G, (g+1)*16/G) and the decode's
+    wide CRT is the RCCL recombine (mfhe_decrypt_and_decode_sharded).  All ranks work on ONE batch (strong
+    scaling inside this line).  Input and check: test_encode_encrypt_decrypt_decode_wcrt.cu:44-52,109."""
+    import numpy as np
+    import torch
+    import mfhe
+    L, G = 16, world
+    if L % G or 512 % G:
+        return {"skipped": f"world {G} does not divide 16 limbs / 512 lanes"}
+    moduli = gen_moduli(35, 197376, L)
+    lg = L // G
+    ctx = mfhe.Context(moduli[rank * lg:(rank + 1) * lg], 6, mfhe.CONV_PHANTOM | mfhe.CONV_WCRT)
+    ctx.set_limb_shard(rank * lg, L)
+    ctx.reserve_workspace()
+    c_all = mfhe.Context(moduli, 6, mfhe.CONV_PHANTOM)
+    n2 = 4096
+    msg = (np.arange(512)[:, None] * np.ones((1, n2)) + 0.001j).ravel()
+    mt = torch.from_numpy(msg.view(np.float64).copy()).cuda()
+    words = 512 * lg * n2
+    re_, im_ = (torch.empty(words, dtype=torch.int64, device="cuda") for _ in range(2))
+    cre, cim = (torch.empty(2 * words, dtype=torch.int64, device="cuda") for _ in range(2))
+    sk = torch.empty(512 * lg * 64, dtype=torch.int64, device="cuda")
+    res = torch.empty_like(mt)
+    ctx.keygen(sk)
+    out = {}
+    for mode in ("allgather", "alltoall"):
+        ctx.decrypt_and_decode_sharded(c_all, comm, mode, cre, cim, sk, res)   # grows the receive buffer
+
+        def run():
+            ctx.encode(mt, re_, im_)
+            ctx.encrypt_pair(re_, im_, sk, cre, cim)
+            ctx.decrypt_and_decode_sharded(c_all, comm, mode, cre, cim, sk, res)
+        run()
+        barrier()
+        t0 = time.perf_counter()
+        for _ in range(reps):
+            run()
+        barrier()
+        dt = (time.perf_counter() - t0) / reps
+        t = torch.tensor([dt], dtype=torch.float64, device="cuda")
+        if world > 1:
+            import torch.distributed as dist
+            dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        err = float(np.max(np.abs(res.cpu().numpy().view(np.complex128) - msg)))
+        out[mode] = {"ms": round(t.item() * 1e3, 3), "messages_per_s": round(512 * n2 / t.item()), "max_err": err,
+                     "check_1e-3": err < 1e-3}
+    ctx.close()
+    c_all.close()
+    return {"workload": f"C4: encode->encrypt_pair->decrypt_and_decode, n=64 x 512 W-lanes, L=16 x 35-bit moduli, "
+                        f"limbs sharded over {G} GPU(s) ({lg} per GPU), RCCL recombine in decode",
+            "scaling": "strong (one batch for all ranks)", **out}
 
 
 def cpu_baseline(log_n, moduli, seconds):
@@ -507,6 +563,16 @@ def main():
                             **{f"{m}_ms": t * 1e3 for m, t in rc.items()},
                             **{f"{m}_polys_per_s": rb / t for m, t in rc.items()}}
 
+    c4 = None
+    if args.only in ("all", "c4") and not args.no_pipeline:
+        if world > 1 and backend == "nccl":
+            c4comm = mfhe.Comm.create()
+        else:
+            c4comm = mfhe.Comm.from_id(mfhe.Comm.unique_id(), 1, 0) if world == 1 else None
+        if c4comm is not None:
+            c4 = c4_line(world, rank, c4comm, barrier)
+            c4comm.close()
+
     if rank == 0:
         ntts = batch * L * world
         out = {
@@ -555,6 +621,8 @@ def main():
             out["encode_crt_GBps"] = 16.0 * (L + 1) * N * cb / (res["crt_ev_ms"] * 1e-3) / 1e9
         if "recombine" in res:
             out["residue_shard_ntt_roundtrip_crt_recombine"] = res["recombine"]
+        if c4 is not None:
+            out["c4_sharded_pipeline"] = c4
         if world == 1 and not args.no_pipeline and args.only == "all":
             out["reference_geometry_pipeline"] = pipeline_line()
             out["other_ntt_configs"] = other_configs_line()

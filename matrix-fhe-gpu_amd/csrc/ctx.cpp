@@ -534,6 +534,16 @@ extern "C" int mfhe_ctx_set_arith(mfhe_ctx* c, int arith) {
     return MFHE_OK;
 }
 
+extern "C" int mfhe_ctx_set_limb_shard(mfhe_ctx* c, int limb_base, int limbs_total) {
+    if (!c) return set_error(MFHE_EINVAL, "mfhe_ctx_set_limb_shard: null ctx");
+    if (limbs_total == 0) limbs_total = c->L;
+    if (limb_base < 0 || limbs_total < c->L || limb_base + c->L > limbs_total)
+        return set_error(MFHE_EINVAL, "mfhe_ctx_set_limb_shard: [limb_base, limb_base + L) must lie in [0, limbs_total)");
+    c->limb_base = limb_base;
+    c->limbs_total = limbs_total;
+    return MFHE_OK;
+}
+
 extern "C" int mfhe_ctx_set_option(mfhe_ctx* c, int opt, int64_t v) {
     if (!c) return set_error(MFHE_EINVAL, "mfhe_ctx_set_option: null ctx");
     switch (opt) {

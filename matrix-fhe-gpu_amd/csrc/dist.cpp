@@ -161,6 +161,22 @@ extern "C" int mfhe_allgather_limbs(mfhe_comm* c, const uint64_t* d_shard, size_
     return e == ncclSuccess ? MFHE_OK : nccl_error(e, "ncclAllGather");
 }
 
+namespace mfhe {
+int comm_allgather_bytes(mfhe_comm* c, const void* send, void* recv, size_t bytes, hipStream_t s) {
+    if (!c) return set_error(MFHE_EINVAL, "null comm");
+    if (bytes == 0) return MFHE_OK;
+    if (int rc = need_rccl()) return rc;
+    ncclResult_t e = rccl().AllGather(send, recv, bytes, ncclUint8, c->comm, s);
+    return e == ncclSuccess ? MFHE_OK : nccl_error(e, "ncclAllGather");
+}
+int comm_size_rank(const mfhe_comm* c, int* size, int* rank) {
+    if (!c) return set_error(MFHE_EINVAL, "null comm");
+    *size = c->nranks;
+    *rank = c->rank;
+    return MFHE_OK;
+}
+}  // namespace mfhe
+
 namespace {
 
 // receive-buffer words of one recombine exchange

@@ -56,12 +56,16 @@ __global__ void ternary_kernel(uint64_t* s, const uint64_t* qmu, int L, int log_
     s[idx] = (r == 0) ? 0 : (r == 1) ? 1 : q - 1;
 }
 
-// uniform_random_kernel HE.cu:564-578, matrix-major [phi][L][n*n]
-__global__ void uniform_kernel(uint64_t* a, const uint64_t* qmu, int L, int log_n, uint64_t total) {
+// uniform_random_kernel HE.cu:564-578, matrix-major [phi][L][n*n].  The seed is the element's index in the
+// WHOLE parameter set ([phi][Ltot][n*n], this context's limb l being global limb lbase + l), so a residue
+// shard (mfhe_ctx_set_limb_shard) draws exactly its limbs of the unsharded a.
+__global__ void uniform_kernel(uint64_t* a, const uint64_t* qmu, int L, int log_n, uint64_t total, int lbase, int Ltot) {
     const uint64_t idx = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x;
     if (idx >= total) return;
-    const int limb = (int)((idx % ((uint64_t)L << (2 * log_n))) >> (2 * log_n));
-    uint64_t seed = 123456789ULL + idx;
+    const uint64_t n2 = 1ull << (2 * log_n), pos = idx & (n2 - 1), wl = idx >> (2 * log_n);
+    const uint64_t w = wl / (uint64_t)L;
+    const int limb = (int)(wl - w * (uint64_t)L);
+    uint64_t seed = 123456789ULL + ((w * (uint64_t)Ltot + (uint64_t)(lbase + limb)) << (2 * log_n)) + pos;
     seed = seed * 6364136223846793005ULL + 1442695040888963407ULL;
     a[idx] = seed % qmu[2 * limb];
 }
@@ -721,7 +725,8 @@ static int encrypt_impl(mfhe_ctx* c, const uint64_t* m_re, const uint64_t* m_im,
     uint64_t* eev = b.get<uint64_t>(g.words);
     const uint64_t W = g.words;
     // shared a: W coeff -> W-CRT eval (poly-major) -> X-NTT
-    hipLaunchKernelGGL(uniform_kernel, g1(W), dim3(256), 0, s, ap, c->d_rns_mu, g.L, g.logn, W);
+    hipLaunchKernelGGL(uniform_kernel, g1(W), dim3(256), 0, s, ap, c->d_rns_mu, g.L, g.logn, W, c->limb_base,
+                       c->limbs_total ? c->limbs_total : g.L);
     MFHE_CHECK_LAUNCH("uniform_kernel");
     RC(wcrt_gemm(c, c->d_wV, ap, false, aev, WOut::Poly, false, s));
     // e: identical for re and im (seed depends only on the coefficient, HE.cu:605-608)
@@ -771,6 +776,33 @@ static int decrypt_impl(mfhe_ctx* c, const uint64_t* ct, const uint64_t* sk, uin
     RC(mfhe_ntt_inv(c, t, 512 * g.n, 0, g.L, (mfhe_stream_t)s));
     hipLaunchKernelGGL(dec_combine_kernel, g1(W), dim3(256), 0, s, ct, t, out, c->d_rns_mu, g.logn, g.L, W);
     MFHE_CHECK_LAUNCH("dec_combine_kernel");
+    return MFHE_OK;
+}
+
+// Residue-sharded decode (BASELINE C4): this rank's W-INTT of its limbs, the RCCL recombine of every lane's
+// L residues (dist.cpp) into this rank's lane slice of the centred / delta values, an all-gather of those
+// f64 slices, then the W-DFT and XY-DFT of the whole batch (FP64, replicated on every rank).  Replaces
+// decode_eval_pair_to_complex (HE.cu:1619-1689) whose per-lane compose loop (:1653-1668) is the exchange step.
+static int decode_sharded_impl(mfhe_ctx* c, mfhe_ctx* call, mfhe_comm* comm, int mode, const uint64_t* ev_re,
+                               const uint64_t* ev_im, double* msg, hipStream_t s, Bump* pb) {
+    const Geo2 g = geo(c);
+    int G = 1, rank = 0;
+    RC(comm_size_rank(comm, &G, &rank));
+    if (512 % G) return set_error(MFHE_EINVAL, "sharded decode: the communicator size must divide 512 lanes");
+    if (call->L != (c->limbs_total ? c->limbs_total : c->L) || call->L != c->L * G)
+        return set_error(MFHE_EINVAL, "sharded decode: ctx_all must hold the G * L_shard moduli of the whole set");
+    uint64_t* coeff = pb->get<uint64_t>(g.words);
+    double2* ccx = pb->get<double2>(g.cnt);
+    double2* ecx = pb->get<double2>(g.cnt);
+    const size_t bs = 512 / G;
+    double2* mine = ccx + (size_t)rank * bs * g.n2;
+    RC(wcrt_gemm(c, c->d_wVinv, ev_re, true, coeff, WOut::Matrix, false, s));
+    RC(mfhe_crt_recombine_sharded(call, comm, mode, coeff, 512, g.n2, (double*)mine, 2, (mfhe_stream_t)s));
+    RC(wcrt_gemm(c, c->d_wVinv, ev_im, true, coeff, WOut::Matrix, false, s));
+    RC(mfhe_crt_recombine_sharded(call, comm, mode, coeff, 512, g.n2, (double*)mine + 1, 2, (mfhe_stream_t)s));
+    RC(comm_allgather_bytes(comm, mine, ccx, bs * g.n2 * sizeof(double2), s));   // in place
+    RC(wdft(c, c->d_wdV, ccx, ecx, s));
+    RC(xy3(c, c->d_encV, ecx, c->d_encVT, ccx, (double2*)msg, 512, s));
     return MFHE_OK;
 }
 
@@ -924,6 +956,40 @@ extern "C" int mfhe_decrypt_and_decode(mfhe_ctx* c, const uint64_t* cre, const u
     RC(decrypt_impl(c, cim, sk, ei, (hipStream_t)s, &inner));
     inner = b;
     return decode_impl(c, er, ei, msg, (hipStream_t)s, &inner);
+}
+
+static int sharded_args(mfhe_ctx* c, mfhe_ctx* call, mfhe_comm* comm, const void* a, const void* b, const void* m) {
+    RC(need_wcrt(c));
+    if (!call || !comm || !a || !b || !m) return set_error(MFHE_EINVAL, "sharded decode: null pointer");
+    if (call->N != c->N) return set_error(MFHE_EINVAL, "sharded decode: ctx_all has another ring degree");
+    return MFHE_OK;
+}
+extern "C" int mfhe_decode_sharded(mfhe_ctx* c, mfhe_ctx* call, mfhe_comm* comm, int mode, const uint64_t* re,
+                                   const uint64_t* im, double* msg, mfhe_stream_t s) {
+    RC(sharded_args(c, call, comm, re, im, msg));
+    RC(ensure_xy(c));
+    RC(ensure_ws(c));
+    Bump b{(char*)c->ws};
+    return decode_sharded_impl(c, call, comm, mode, re, im, msg, (hipStream_t)s, &b);
+}
+extern "C" int mfhe_decrypt_and_decode_sharded(mfhe_ctx* c, mfhe_ctx* call, mfhe_comm* comm, int mode,
+                                               const uint64_t* cre, const uint64_t* cim, const uint64_t* sk, double* msg,
+                                               mfhe_stream_t s) {
+    RC(sharded_args(c, call, comm, cre, cim, msg));
+    if (!(c->conv & MFHE_CONV_PHANTOM)) return set_error(MFHE_ENOTREADY, "decrypt needs MFHE_CONV_PHANTOM (X-NTT)");
+    if (!sk) return set_error(MFHE_EINVAL, "sharded decrypt: null key");
+    RC(ensure_xy(c));
+    RC(ensure_ws(c));
+    const Geo2 g = geo(c);
+    Bump b{(char*)c->ws};
+    uint64_t* er = b.get<uint64_t>(g.words);
+    uint64_t* ei = b.get<uint64_t>(g.words);
+    Bump inner = b;
+    RC(decrypt_impl(c, cre, sk, er, (hipStream_t)s, &inner));
+    inner = b;
+    RC(decrypt_impl(c, cim, sk, ei, (hipStream_t)s, &inner));
+    inner = b;
+    return decode_sharded_impl(c, call, comm, mode, er, ei, msg, (hipStream_t)s, &inner);
 }
 
 static int wdft_pair(mfhe_ctx* c, const void* re, const void* im, bool i64, double* ore, double* oim, bool inv,

@@ -18,6 +18,9 @@ namespace mfhe {
 
 // thread-local error reporting
 int set_error(int code, const std::string& msg);
+// dist.cpp: in-place-capable all-gather of `bytes` per rank over a libmfhe communicator (RCCL)
+int comm_allgather_bytes(mfhe_comm* comm, const void* send, void* recv, size_t bytes, hipStream_t s);
+int comm_size_rank(const mfhe_comm* comm, int* size, int* rank);
 int hip_error(hipError_t e, const char* what);
 int ensure_xy(mfhe_ctx* c);   // XY encoder matrices, built on first use (ctx.cpp)
 
@@ -90,6 +93,8 @@ struct mfhe_ctx {
     int wcrt_mfma = 1;           // MFHE_OPT_WCRT_MFMA
     int cgemm_mfma = 1;          // MFHE_OPT_CGEMM_MFMA
     int he_fused = 1;            // MFHE_OPT_HE_FUSED
+    int limb_base = 0;           // residue shard: global index of this context's limb 0 (mfhe_ctx_set_limb_shard)
+    int limbs_total = 0;         // residue shard: L of the whole parameter set (0 = this context's L)
     void* gemm_ws = nullptr;     // B digit planes for the MFMA GEMM, grown on demand
     size_t gemm_ws_bytes = 0;
     size_t fused_bytes = 0;

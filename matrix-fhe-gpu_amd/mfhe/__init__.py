@@ -124,6 +124,9 @@ _sig("mfhe_comm_info", [_vp, ctypes.POINTER(ctypes.c_int), ctypes.POINTER(ctypes
 _sig("mfhe_allgather_limbs", [_vp, _vp, _sz, _vp, _vp])
 _sig("mfhe_crt_recombine_sharded", [_vp, _vp, ctypes.c_int, _vp, _sz, _sz, _vp, _sz, _vp])
 _sig("mfhe_crt_recombine_reserve", [_vp, _vp, ctypes.c_int, _sz, _sz])
+_sig("mfhe_ctx_set_limb_shard", [_vp, ctypes.c_int, ctypes.c_int])
+_sig("mfhe_decode_sharded", [_vp, _vp, _vp, ctypes.c_int, _vp, _vp, _vp, _vp])
+_sig("mfhe_decrypt_and_decode_sharded", [_vp, _vp, _vp, ctypes.c_int, _vp, _vp, _vp, _vp, _vp])
 _sig("mfhe_last_error", [], ctypes.c_char_p)
 _sig("mfhe_version", [], ctypes.c_char_p)
 
@@ -153,6 +156,20 @@ def _need(t, words, what):
         raise ValueError(f"{what}: {t.numel()} elements of {t.element_size()} B < {words} words needed")
 
 
+class _stdout_to_stderr:
+    """RCCL's initialisation banner goes to fd 1; keep a caller's stdout (bench.py's one JSON line) clean."""
+
+    def __enter__(self):
+        import sys
+        sys.stdout.flush()
+        self._saved = os.dup(1)
+        os.dup2(2, 1)
+
+    def __exit__(self, *exc):
+        os.dup2(self._saved, 1)
+        os.close(self._saved)
+
+
 class Comm:
     """An RCCL communicator owned by libmfhe (include/mfhe.h mfhe_comm_*): one per process/GPU.
 
@@ -166,13 +183,17 @@ class Comm:
     def from_id(cls, uid: bytes, world: int, rank: int) -> "Comm":
         buf = (ctypes.c_uint8 * COMM_ID_BYTES).from_buffer_copy(uid)
         h = _vp()
-        check(lib.mfhe_comm_init(ctypes.addressof(buf), world, rank, ctypes.byref(h)), "comm_init")
+        with _stdout_to_stderr():
+            rc = lib.mfhe_comm_init(ctypes.addressof(buf), world, rank, ctypes.byref(h))
+        check(rc, "comm_init")
         return cls(h, world, rank)
 
     @staticmethod
     def unique_id() -> bytes:
         buf = (ctypes.c_uint8 * COMM_ID_BYTES)()
-        check(lib.mfhe_comm_unique_id(ctypes.addressof(buf)), "comm_unique_id")
+        with _stdout_to_stderr():
+            rc = lib.mfhe_comm_unique_id(ctypes.addressof(buf))
+        check(rc, "comm_unique_id")
         return bytes(buf)
 
     @classmethod
@@ -415,6 +436,23 @@ class Context:
         self._call("mfhe_decrypt_to_eval", _ptr(ct), _ptr(sk), _ptr(out), stream=stream); return out
     def decrypt_and_decode(self, ct_re, ct_im, sk, msg, stream=None):
         self._call("mfhe_decrypt_and_decode", _ptr(ct_re), _ptr(ct_im), _ptr(sk), _ptr(msg), stream=stream); return msg
+
+    # ---- residue sharding across GPUs (BASELINE C4, include/mfhe.h) ----
+    def set_limb_shard(self, limb_base: int, limbs_total: int):
+        """This context holds limbs [limb_base, limb_base + L) of a limbs_total-modulus parameter set."""
+        check(lib.mfhe_ctx_set_limb_shard(self._h, limb_base, limbs_total), "set_limb_shard")
+
+    def decode_sharded(self, ctx_all: "Context", comm: "Comm", mode, ev_re, ev_im, msg, stream=None):
+        m = _XCHG[mode] if isinstance(mode, str) else mode
+        check(lib.mfhe_decode_sharded(self._h, ctx_all._h, comm._h, m, _ptr(ev_re), _ptr(ev_im), _ptr(msg),
+                                      _stream_ptr(stream)), "decode_sharded")
+        return msg
+
+    def decrypt_and_decode_sharded(self, ctx_all: "Context", comm: "Comm", mode, ct_re, ct_im, sk, msg, stream=None):
+        m = _XCHG[mode] if isinstance(mode, str) else mode
+        check(lib.mfhe_decrypt_and_decode_sharded(self._h, ctx_all._h, comm._h, m, _ptr(ct_re), _ptr(ct_im), _ptr(sk),
+                                                  _ptr(msg), _stream_ptr(stream)), "decrypt_and_decode_sharded")
+        return msg
 
 
 def fnwt_1d(data, tw, tw_shoup, dmod, dim, coeff_modulus_size, start_modulus_idx=0, batch=1, stream=None):

@@ -84,3 +84,54 @@ def test_limb_range_rejects_uneven():
     assert mdist.limb_range(8, 4, 3) == (6, 2)
     with pytest.raises(ValueError):
         mdist.limb_range(6, 4, 0)
+
+
+def _c4_rank(rank, world, port, mode, q):
+    """BASELINE C4 decode exchange: 16 limbs over `world` ranks, every rank composes its lane slice and an
+    all-gather of the f64 slices gives every rank the whole batch (mfhe_decode_sharded's data flow)."""
+    import sys
+    from pathlib import Path
+    root = Path(__file__).resolve().parent.parent
+    sys.path[:0] = [str(root / "matrix-fhe-gpu_amd"), str(root / "tests")]
+    import torch.distributed as dist
+    from mfhe import dist as mdist
+    import oracle as O
+
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        moduli = O.gen_primes(35, 197376, 16)
+        lanes, n2 = 8, 16
+        rng = np.random.default_rng(5)
+        v = rng.integers(-(1 << 40), 1 << 40, (lanes, n2))
+        full = np.stack([(v.astype(object) % m).astype(np.uint64) for m in moduli], axis=1)   # [lanes][16][n2]
+        s0, lg = mdist.limb_range(16, world, rank)
+        shard = torch.from_numpy(full[:, s0:s0 + lg, :].astype(np.int64).copy())
+        buf, off, stride, bs = mdist.exchange_residues(shard, lanes, lg, n2, mode)
+        b = buf.numpy().view(np.uint64)
+        view = np.stack([b[off + s * stride: off + s * stride + bs * lg * n2].reshape(bs, lg, n2)
+                         for s in range(world)], axis=1).reshape(bs, 16, n2)
+        W = O.crt_words(moduli)
+        mag, neg = O.crt_compose(view.ravel(), bs, 16, n2, moduli, W)
+        mine = torch.from_numpy(O.big_to_f64(mag, neg, W, 2.0 ** 35))
+        slices = [torch.empty_like(mine) for _ in range(world)]
+        dist.all_gather(slices, mine)
+        got = torch.cat(slices).numpy()
+        q.put((rank, bool(np.array_equal(got, v.ravel().astype(np.float64) / 2.0 ** 35))))
+    finally:
+        dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("world", [2, 4])
+@pytest.mark.parametrize("mode", ["allgather", "alltoall"])
+def test_c4_decode_exchange(mode, world):
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_c4_rank, args=(r, world, port, mode, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    res = dict(q.get(timeout=120) for _ in procs)
+    for p in procs:
+        p.join(timeout=60)
+    assert res == {r: True for r in range(world)}
