@@ -133,9 +133,6 @@ struct mfhe_ctx {
     double2* d_wdVinv = nullptr;   // [512][512]     its inverse (complex Gauss-Jordan)
     double2 *d_encV = nullptr, *d_encVT = nullptr, *d_encVi = nullptr, *d_encViT = nullptr;  // [n][n]
 
-    // trace GEMM (trace.hip): n mod q_l, centred, for the FP64 epilogue; built on first use for trace_n
-    double* d_trace_nmod = nullptr;   // [L][3]: n, 2^S, 2^2S mod q_l (centred)
-    int trace_n = 0, trace_s = 0;
     int trace_split = 2;              // MFHE_OPT_TRACE_SPLIT: split-digit kernel (2 MFMA, 1 VALU) when every q < 2^45
 
     // pipeline workspace (allocated on first use / mfhe_ctx_reserve_workspace)

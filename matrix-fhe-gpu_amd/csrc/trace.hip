@@ -40,6 +40,14 @@ __device__ __forceinline__ uint64_t tr_mod128(unsigned __int128 v, uint64_t q, u
 }
 
 // map_Bprime_batched_kernel (batched_trace.cu:37-79): conj(B), row j -> (n - j) mod n, rows j != 0 times -i.
+
+// Per-limb epilogue constants, centred: n, 2^S, 2^2S mod q_l (S = the digit split).  Passed by value in the
+// kernel arguments, so concurrent calls with different n / S on different streams never share mutable state.
+constexpr int kTraceMaxLimbs = 64;
+struct TraceK {
+    double k[3 * kTraceMaxLimbs];
+};
+
 __global__ void trace_map_kernel(const uint64_t* __restrict__ br, const uint64_t* __restrict__ bi,
                                  uint64_t* __restrict__ opr, uint64_t* __restrict__ opi, const uint64_t* qmu,
                                  int log_n, int L, uint64_t total) {
@@ -63,7 +71,7 @@ template <int KR>
 __global__ __launch_bounds__(256) void trace_gemm_f64_kernel(
     const uint64_t* __restrict__ Ar, const uint64_t* __restrict__ Ai, const uint64_t* __restrict__ Br,
     const uint64_t* __restrict__ Bi, uint64_t* __restrict__ Cr, uint64_t* __restrict__ Ci,
-    const LimbConst* __restrict__ lf, const double* __restrict__ nmod, int log_n, int L) {
+    const LimbConst* __restrict__ lf, TraceK kc, int log_n, int L) {
     __shared__ double sA[2][TR_KP][TR_LDS];
     __shared__ double sB[2][TR_KP][TR_LDS];
     const int n = 1 << log_n, tdim = n / TR_TILE, tiles = tdim * tdim;
@@ -128,7 +136,7 @@ __global__ __launch_bounds__(256) void trace_gemm_f64_kernel(
         }
         __syncthreads();
     }
-    const double nm = nmod[3 * l];   // n mod q, centred
+    const double nm = kc.k[3 * l];   // n mod q, centred
 #pragma unroll
     for (int i = 0; i < 4; ++i)
 #pragma unroll
@@ -149,7 +157,7 @@ __global__ __launch_bounds__(256) void trace_gemm_f64_kernel(
 __global__ __launch_bounds__(512) void trace_gemm_split_kernel(
     const uint64_t* __restrict__ Ar, const uint64_t* __restrict__ Ai, const uint64_t* __restrict__ Br,
     const uint64_t* __restrict__ Bi, uint64_t* __restrict__ Cr, uint64_t* __restrict__ Ci,
-    const LimbConst* __restrict__ lf, const double* __restrict__ consts, int log_n, int L, double two_s,
+    const LimbConst* __restrict__ lf, TraceK kc, int log_n, int L, double two_s,
     double inv_two_s) {
     // [re hi, re lo, im hi, im lo][k][row]
     __shared__ double sA[4][TR_KP][TR_LDS];
@@ -230,7 +238,7 @@ __global__ __launch_bounds__(512) void trace_gemm_split_kernel(
                 }
         }
     }
-    const double nm = consts[3 * l], c1 = consts[3 * l + 1], c2 = consts[3 * l + 2];   // centred n, 2^S, 2^2S mod q
+    const double nm = kc.k[3 * l], c1 = kc.k[3 * l + 1], c2 = kc.k[3 * l + 2];   // centred n, 2^S, 2^2S mod q
 #pragma unroll
     for (int i = 0; i < 4; ++i)
 #pragma unroll
@@ -265,7 +273,7 @@ template <bool FUSE>
 __global__ __launch_bounds__(512) void trace_gemm_split_mfma_kernel(
     const uint64_t* __restrict__ Ar, const uint64_t* __restrict__ Ai, const uint64_t* __restrict__ Br,
     const uint64_t* __restrict__ Bi, uint64_t* __restrict__ Cr, uint64_t* __restrict__ Ci,
-    const LimbConst* __restrict__ lf, const double* __restrict__ consts, int log_n, int L, double two_s,
+    const LimbConst* __restrict__ lf, TraceK kc, int log_n, int L, double two_s,
     double inv_two_s, TracePost post) {
     // planes: 0 re hi, 1 re lo, 2 im hi, 3 im lo
     __shared__ double sA[4][TR_TILE * TR_CAP];
@@ -381,7 +389,7 @@ __global__ __launch_bounds__(512) void trace_gemm_split_mfma_kernel(
                     for (int g = 0; g < 4; ++g) acc[j][t][g] = ar.reduce(acc[j][t][g]);
         }
     }
-    const double nm = FUSE ? post.f[l] : consts[3 * l], c1 = consts[3 * l + 1], c2 = consts[3 * l + 2];
+    const double nm = FUSE ? post.f[l] : kc.k[3 * l], c1 = kc.k[3 * l + 1], c2 = kc.k[3 * l + 2];
 #pragma unroll
     for (int j = 0; j < 2; ++j)
 #pragma unroll
@@ -462,6 +470,19 @@ int trace_check(const mfhe_ctx* c, int n, int nlimbs, size_t batch, const char* 
 
 int ilog2(int n) { return 31 - __builtin_clz((unsigned)n); }
 
+TraceK trace_consts(const mfhe_ctx* c, int n, int S, int nlimbs) {
+    auto centred = [](uint64_t v, uint64_t q) { return v > q / 2 ? (double)v - (double)q : (double)v; };
+    TraceK k{};
+    for (int l = 0; l < nlimbs && l < kTraceMaxLimbs; ++l) {
+        const uint64_t q = c->moduli[l];
+        const uint64_t t1 = (uint64_t)(((unsigned __int128)1 << S) % q);
+        k.k[3 * l] = centred((uint64_t)n % q, q);
+        k.k[3 * l + 1] = centred(t1, q);
+        k.k[3 * l + 2] = centred((uint64_t)((unsigned __int128)t1 * t1 % q), q);
+    }
+    return k;
+}
+
 }  // namespace
 }  // namespace mfhe
 
@@ -485,55 +506,40 @@ extern "C" int mfhe_trace_gemm(mfhe_ctx* c, const uint64_t* ar, const uint64_t* 
                                mfhe_stream_t s) {
     if (int rc = trace_check(c, n, nlimbs, batch, "mfhe_trace_gemm")) return rc;
     if (!ar || !ai || !bpr || !bpi || !cr || !ci) return set_error(MFHE_EINVAL, "mfhe_trace_gemm: null pointer");
+    for (const uint64_t* o : {cr, ci})
+        if (o == ar || o == ai || o == bpr || o == bpi)
+            return set_error(MFHE_EINVAL, "mfhe_trace_gemm: outputs must not overlap the inputs (other tiles still read them)");
     const uint64_t total = (uint64_t)batch * nlimbs * n * n;
     const int log_n = ilog2(n);
-    if (c->f64_ok && n % TR_TILE == 0) {
+    if (c->f64_ok && n % TR_TILE == 0 && nlimbs <= kTraceMaxLimbs) {
         uint64_t qmax = 0;
         for (int l = 0; l < nlimbs; ++l) qmax = c->moduli[l] > qmax ? c->moduli[l] : qmax;
         const int qbits = 64 - __builtin_clzll(qmax);
         const int S = (qbits + 1) / 2;
         const bool split = c->trace_split && qbits <= 45;
-        if (!c->d_trace_nmod || c->trace_n != n || c->trace_s != S) {
-            // per limb, centred: n mod q, 2^S mod q, 2^2S mod q (rebuilt when n or S changes)
-            if (!c->d_trace_nmod) {
-                MFHE_HIP(hipMalloc(&c->d_trace_nmod, sizeof(double) * 3 * c->L));
-                c->allocs.push_back(c->d_trace_nmod);
-            }
-            auto centred = [](uint64_t v, uint64_t q) { return v > q / 2 ? (double)v - (double)q : (double)v; };
-            std::vector<double> k(3 * c->L);
-            for (int l = 0; l < c->L; ++l) {
-                const uint64_t q = c->moduli[l];
-                const uint64_t t1 = (uint64_t)(((unsigned __int128)1 << S) % q);
-                k[3 * l] = centred((uint64_t)n % q, q);
-                k[3 * l + 1] = centred(t1, q);
-                k[3 * l + 2] = centred((uint64_t)((unsigned __int128)t1 * t1 % q), q);
-            }
-            MFHE_HIP(hipMemcpy(c->d_trace_nmod, k.data(), sizeof(double) * 3 * c->L, hipMemcpyHostToDevice));
-            c->trace_n = n;
-            c->trace_s = S;
-        }
+        const TraceK kc = trace_consts(c, n, S, nlimbs);
         const uint64_t blocks = (uint64_t)batch * nlimbs * (n / TR_TILE) * (n / TR_TILE);
         if (blocks > 0x7fffffffull) return set_error(MFHE_EINVAL, "mfhe_trace_gemm: batch too large");
         if (split && c->trace_split == 2) {
             hipLaunchKernelGGL(trace_gemm_split_mfma_kernel<false>, dim3((uint32_t)blocks), dim3(512), 0,
-                               (hipStream_t)s, ar, ai, bpr, bpi, cr, ci, c->d_limbs, c->d_trace_nmod, log_n, nlimbs,
+                               (hipStream_t)s, ar, ai, bpr, bpi, cr, ci, c->d_limbs, kc, log_n, nlimbs,
                                std::ldexp(1.0, S), std::ldexp(1.0, -S), TracePost{});
             MFHE_CHECK_LAUNCH("trace_gemm_split_mfma_kernel");
             return MFHE_OK;
         }
         if (split) {
             hipLaunchKernelGGL(trace_gemm_split_kernel, dim3((uint32_t)blocks), dim3(512), 0, (hipStream_t)s, ar, ai,
-                               bpr, bpi, cr, ci, c->d_limbs, c->d_trace_nmod, log_n, nlimbs, std::ldexp(1.0, S),
+                               bpr, bpi, cr, ci, c->d_limbs, kc, log_n, nlimbs, std::ldexp(1.0, S),
                                std::ldexp(1.0, -S));
             MFHE_CHECK_LAUNCH("trace_gemm_split_kernel");
             return MFHE_OK;
         }
         if ((double)qmax * 48.5 < 9007199254740992.0)   // (0.5 + 3 * 16) q < 2^53
             hipLaunchKernelGGL(trace_gemm_f64_kernel<16>, dim3((uint32_t)blocks), dim3(256), 0, (hipStream_t)s, ar,
-                               ai, bpr, bpi, cr, ci, c->d_limbs, c->d_trace_nmod, log_n, nlimbs);
+                               ai, bpr, bpi, cr, ci, c->d_limbs, kc, log_n, nlimbs);
         else
             hipLaunchKernelGGL(trace_gemm_f64_kernel<2>, dim3((uint32_t)blocks), dim3(256), 0, (hipStream_t)s, ar,
-                               ai, bpr, bpi, cr, ci, c->d_limbs, c->d_trace_nmod, log_n, nlimbs);
+                               ai, bpr, bpi, cr, ci, c->d_limbs, kc, log_n, nlimbs);
         MFHE_CHECK_LAUNCH("trace_gemm_f64_kernel");
         return MFHE_OK;
     }
@@ -566,33 +572,17 @@ extern "C" int mfhe_trace_product(mfhe_ctx* c, const uint64_t* ar, const uint64_
                                   const uint64_t* inv, mfhe_stream_t s) {
     if (int rc = trace_check(c, n, nlimbs, batch, "mfhe_trace_product")) return rc;
     if (!ar || !ai || !br || !bi || !cr || !ci) return set_error(MFHE_EINVAL, "mfhe_trace_product: null pointer");
-    if (cr == br || cr == bi || ci == br || ci == bi)
-        return set_error(MFHE_EINVAL, "mfhe_trace_product: output must not alias B");
+    for (const uint64_t* o : {cr, ci})
+        if (o == ar || o == ai || o == br || o == bi)
+            return set_error(MFHE_EINVAL, "mfhe_trace_product: outputs must not overlap the inputs (other tiles still read them)");
     uint64_t qmax = 0;
     for (int l = 0; l < nlimbs; ++l) qmax = c->moduli[l] > qmax ? c->moduli[l] : qmax;
-    if (!c->f64_ok || n % TR_TILE != 0 || 64 - __builtin_clzll(qmax) > 45 || nlimbs > 64)
+    if (!c->f64_ok || n % TR_TILE != 0 || 64 - __builtin_clzll(qmax) > 45 || nlimbs > kTraceMaxLimbs)
         return set_error(MFHE_EUNSUPPORTED, "mfhe_trace_product: needs n % 64 == 0, every q < 2^45, nlimbs <= 64 "
                                             "(use mfhe_trace_map_bprime + mfhe_trace_gemm + mfhe_trace_rescale)");
     // per-limb constants for this n and digit split (same table as mfhe_trace_gemm)
     const int qbits = 64 - __builtin_clzll(qmax), S = (qbits + 1) / 2;
-    if (!c->d_trace_nmod || c->trace_n != n || c->trace_s != S) {
-        if (!c->d_trace_nmod) {
-            MFHE_HIP(hipMalloc(&c->d_trace_nmod, sizeof(double) * 3 * c->L));
-            c->allocs.push_back(c->d_trace_nmod);
-        }
-        auto centred = [](uint64_t v, uint64_t q) { return v > q / 2 ? (double)v - (double)q : (double)v; };
-        std::vector<double> k(3 * c->L);
-        for (int l = 0; l < c->L; ++l) {
-            const uint64_t q = c->moduli[l];
-            const uint64_t t1 = (uint64_t)(((unsigned __int128)1 << S) % q);
-            k[3 * l] = centred((uint64_t)n % q, q);
-            k[3 * l + 1] = centred(t1, q);
-            k[3 * l + 2] = centred((uint64_t)((unsigned __int128)t1 * t1 % q), q);
-        }
-        MFHE_HIP(hipMemcpy(c->d_trace_nmod, k.data(), sizeof(double) * 3 * c->L, hipMemcpyHostToDevice));
-        c->trace_n = n;
-        c->trace_s = S;
-    }
+    const TraceK kc = trace_consts(c, n, S, nlimbs);
     TracePost post{};
     for (int l = 0; l < nlimbs; ++l) {
         const uint64_t q = c->moduli[l], nm = (uint64_t)n % q;
@@ -602,7 +592,7 @@ extern "C" int mfhe_trace_product(mfhe_ctx* c, const uint64_t* ar, const uint64_
     const uint64_t blocks = (uint64_t)batch * nlimbs * (n / TR_TILE) * (n / TR_TILE);
     if (blocks > 0x7fffffffull) return set_error(MFHE_EINVAL, "mfhe_trace_product: batch too large");
     hipLaunchKernelGGL(trace_gemm_split_mfma_kernel<true>, dim3((uint32_t)blocks), dim3(512), 0, (hipStream_t)s, ar,
-                       ai, br, bi, cr, ci, c->d_limbs, c->d_trace_nmod, ilog2(n), nlimbs, std::ldexp(1.0, S),
+                       ai, br, bi, cr, ci, c->d_limbs, kc, ilog2(n), nlimbs, std::ldexp(1.0, S),
                        std::ldexp(1.0, -S), post);
     MFHE_CHECK_LAUNCH("trace_gemm_split_mfma_kernel<fused>");
     return MFHE_OK;

@@ -401,17 +401,31 @@ class Context:
     def ct_mul_tensor(self, ct1, ct2, d0, d1, d2, stream=None):
         self._call("mfhe_ct_mul_tensor", _ptr(ct1), _ptr(ct2), _ptr(d0), _ptr(d1), _ptr(d2), stream=stream)
     # ---- trace GEMM, planes [batch][nlimbs][n][n] (batched_trace.cu) ----
+    @staticmethod
+    def _trace_need(tensors, n, nlimbs, batch, what):
+        """Every plane must hold batch * nlimbs * n * n int64/uint64 words (checked before raw pointers cross)."""
+        import torch
+        words = batch * nlimbs * n * n
+        for t in tensors:
+            if t.dtype not in (torch.int64, torch.uint64):
+                raise ValueError(f"{what}: planes must be int64/uint64, got {t.dtype}")
+            _need(t, words, what)
+
     def trace_map_bprime(self, b_re, b_im, bp_re, bp_im, n, nlimbs, batch, stream=None):
+        self._trace_need((b_re, b_im, bp_re, bp_im), n, nlimbs, batch, "trace_map_bprime")
         check(lib.mfhe_trace_map_bprime(self._h, _ptr(b_re), _ptr(b_im), _ptr(bp_re), _ptr(bp_im), n, nlimbs, batch,
                                         _stream_ptr(stream)), "trace_map_bprime")
     def trace_gemm(self, a_re, a_im, bp_re, bp_im, c_re, c_im, n, nlimbs, batch, stream=None):
+        self._trace_need((a_re, a_im, bp_re, bp_im, c_re, c_im), n, nlimbs, batch, "trace_gemm")
         check(lib.mfhe_trace_gemm(self._h, _ptr(a_re), _ptr(a_im), _ptr(bp_re), _ptr(bp_im), _ptr(c_re), _ptr(c_im),
                                   n, nlimbs, batch, _stream_ptr(stream)), "trace_gemm")
     def trace_rescale(self, c_re, c_im, n, nlimbs, batch, inv, stream=None):
+        self._trace_need((c_re, c_im), n, nlimbs, batch, "trace_rescale")
         arr = (ctypes.c_uint64 * nlimbs)(*[int(v) for v in inv[:nlimbs]])
         check(lib.mfhe_trace_rescale(self._h, _ptr(c_re), _ptr(c_im), n, nlimbs, batch, arr, _stream_ptr(stream)),
               "trace_rescale")
     def trace_product(self, a_re, a_im, b_re, b_im, c_re, c_im, n, nlimbs, batch, inv=None, stream=None):
+        self._trace_need((a_re, a_im, b_re, b_im, c_re, c_im), n, nlimbs, batch, "trace_product")
         arr = (ctypes.c_uint64 * nlimbs)(*[int(v) for v in inv[:nlimbs]]) if inv is not None else None
         check(lib.mfhe_trace_product(self._h, _ptr(a_re), _ptr(a_im), _ptr(b_re), _ptr(b_im), _ptr(c_re), _ptr(c_im),
                                      n, nlimbs, batch, arr, _stream_ptr(stream)), "trace_product")

@@ -133,8 +133,9 @@ def test_trace_invalid_arguments(mfhe):
     t = torch.zeros(64 * 64, dtype=torch.int64, device="cuda")
     with pytest.raises(mfhe.MfheError):
         ctx.trace_gemm(t, t, t, t, t, t, 48, 1, 1)        # n not a power of two
+    big = [torch.zeros(12 * 64 * 64, dtype=torch.int64, device="cuda") for _ in range(6)]
     with pytest.raises(mfhe.MfheError):
-        ctx.trace_gemm(t, t, t, t, t, t, 64, 12, 1)       # more limbs than the context
+        ctx.trace_gemm(*big, 64, 12, 1)                   # more limbs than the context
     with pytest.raises(mfhe.MfheError):
         ctx.trace_map_bprime(t, t, t, t, 64, 1, 1)        # aliasing output
 
@@ -173,3 +174,87 @@ def test_trace_product_unsupported_shapes(mfhe, orc):
     ctx2 = mfhe.Context(RNS, 6, mfhe.CONV_PHANTOM)
     with pytest.raises(mfhe.MfheError):
         ctx2.trace_product(t, t, t, t, o, o, 32, 2, 1)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("split", [2, 1])
+@pytest.mark.parametrize("case", ["real", "imag"])
+def test_trace_split_accumulator_bound_45bit(mfhe, orc, split, case):
+    """Split-digit accumulators near their < 2^53 bound: 45-bit primes, operands +-(q-1)/2 with signs that make
+    every digit product of the real (or imaginary) accumulators the same sign, n = 1024 (16 reduction
+    intervals).  Constant planes give the exact answer analytically: C[i][j] = n * n * a * b'_j mod q."""
+    import torch
+    moduli = orc.gen_primes(45, 4, 2)
+    ctx = mfhe.Context(moduli, 1, mfhe.CONV_PHANTOM)
+    ctx.set_option(mfhe.OPT_TRACE_SPLIT, split)
+    n, L, batch = 1024, 2, 1
+
+    def plane(vals):   # vals[l] -> one constant per limb, as canonical residues
+        return np.concatenate([np.full(n * n, v % q, dtype=np.uint64) for v, q in zip(vals, moduli)])
+    X = [(q - 1) // 2 for q in moduli]
+    a = [(x, -x) for x in X] if case == "real" else [(x, x) for x in X]
+    bp = [(x, x) for x in X]
+    d = [mfhe.to_device_u64(plane([v[i] for v in vals])) for vals in (a, bp) for i in (0, 1)]
+    c = [torch.empty_like(d[0]), torch.empty_like(d[0])]
+    ctx.trace_gemm(d[0], d[1], d[2], d[3], c[0], c[1], n, L, batch)
+    torch.cuda.synchronize()
+    for l, q in enumerate(moduli):
+        (ar, ai), (br, bi) = a[l], bp[l]
+        er, ei = n * n * (ar * br - ai * bi) % q, n * n * (ar * bi + ai * br) % q
+        assert np.all(mfhe.to_host_u64(c[0]).reshape(L, -1)[l] == er)
+        assert np.all(mfhe.to_host_u64(c[1]).reshape(L, -1)[l] == ei)
+    # the fused product maps B -> B' itself: B' row 0 = conj(b), rows j != 0 = -i conj(b) = (-b_im, -b_re)
+    if split == 2:
+        b = a     # take B = a's constants; B' then has the mixed signs of the map
+        db = [mfhe.to_device_u64(plane([v[i] for v in b])) for i in (0, 1)]
+        ctx.trace_product(d[0], d[1], db[0], db[1], c[0], c[1], n, L, batch)
+        torch.cuda.synchronize()
+        for l, q in enumerate(moduli):
+            (ar, ai), (br, bi) = a[l], b[l]
+            hr = mfhe.to_host_u64(c[0]).reshape(L, n, n)[l]
+            hi = mfhe.to_host_u64(c[1]).reshape(L, n, n)[l]
+            for j, (pr, pi) in ((0, (br, -bi)), (1, (-bi, -br)), (n - 1, (-bi, -br))):
+                assert np.all(hr[:, j] == n * n * (ar * pr - ai * pi) % q)
+                assert np.all(hi[:, j] == n * n * (ar * pi + ai * pr) % q)
+    ctx.close()
+
+
+@pytest.mark.gpu
+def test_trace_alternating_n_on_side_stream(mfhe, orc):
+    """Calls with different n (hence different per-limb epilogue constants) queued back to back on a side
+    stream with no synchronisation in between: each result must match the oracle (the constants travel in the
+    kernel arguments, no shared device table is rewritten between launches)."""
+    import torch
+    ctx = mfhe.Context(RNS, 6, mfhe.CONV_PHANTOM)
+    L, batch = 3, 2
+    rng = np.random.default_rng(11)
+    st = torch.cuda.Stream()
+    jobs = []
+    with torch.cuda.stream(st):
+        for n in (64, 128, 64, 128):
+            ar, ai, br, bi = (_rand(rng, batch, L, n, RNS) for _ in range(4))
+            d = [mfhe.to_device_u64(x) for x in (ar, ai, br, bi)]
+            c = [torch.empty_like(d[0]), torch.empty_like(d[0])]
+            ctx.trace_gemm(d[0], d[1], d[2], d[3], c[0], c[1], n, L, batch, stream=st)
+            jobs.append((n, (ar, ai, br, bi), c, d))
+    st.synchronize()
+    for n, (ar, ai, br, bi), c, _ in jobs:
+        ocr, oci = orc.trace_gemm(ar, ai, br, bi, n, L, batch, RNS)
+        np.testing.assert_array_equal(mfhe.to_host_u64(c[0]), ocr)
+        np.testing.assert_array_equal(mfhe.to_host_u64(c[1]), oci)
+    ctx.close()
+
+
+@pytest.mark.gpu
+def test_trace_rejects_aliasing_and_short_planes(mfhe):
+    import torch
+    ctx = mfhe.Context(RNS, 6, mfhe.CONV_PHANTOM)
+    n, L, batch = 64, 2, 1
+    p = [torch.zeros(batch * L * n * n, dtype=torch.int64, device="cuda") for _ in range(6)]
+    with pytest.raises(mfhe.MfheError):      # C == A: other tiles still read A
+        ctx.trace_gemm(p[0], p[1], p[2], p[3], p[0], p[5], n, L, batch)
+    with pytest.raises(mfhe.MfheError):
+        ctx.trace_product(p[0], p[1], p[2], p[3], p[4], p[1], n, L, batch)
+    with pytest.raises(ValueError):          # undersized plane caught on the host
+        ctx.trace_gemm(p[0][:100], p[1], p[2], p[3], p[4], p[5], n, L, batch)
+    ctx.close()
