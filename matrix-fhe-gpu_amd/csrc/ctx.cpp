@@ -563,6 +563,10 @@ extern "C" int mfhe_ctx_set_option(mfhe_ctx* c, int opt, int64_t v) {
             if (v < 0 || v > 1) return set_error(MFHE_EINVAL, "prefetch must be 0 or 1");
             c->ntt_prefetch = (int)v;
             return MFHE_OK;
+        case MFHE_OPT_NTT_PACK:
+            if (v < 0 || v > 1) return set_error(MFHE_EINVAL, "pack must be 0 or 1");
+            c->ntt_pack = (int)v;
+            return MFHE_OK;
         case MFHE_OPT_NTT_FUSED:
             if (v < 0 || v > 1) return set_error(MFHE_EINVAL, "fused must be 0 or 1");
             c->ntt_fused = (int)v;
@@ -622,6 +626,7 @@ extern "C" int mfhe_ctx_get_option(const mfhe_ctx* c, int opt, int64_t* v) {
         case MFHE_OPT_NTT_WG_PER_CU: *v = c->ntt_wg_per_cu; return MFHE_OK;
         case MFHE_OPT_NTT_PREFETCH: *v = c->ntt_prefetch; return MFHE_OK;
         case MFHE_OPT_NTT_FUSED: *v = c->ntt_fused; return MFHE_OK;
+        case MFHE_OPT_NTT_PACK: *v = c->ntt_pack; return MFHE_OK;
         case MFHE_OPT_WCRT_MFMA: *v = c->d_wVdig ? c->wcrt_mfma : 0; return MFHE_OK;
         case MFHE_OPT_CGEMM_MFMA: *v = c->cgemm_mfma; return MFHE_OK;
         case MFHE_OPT_HE_FUSED: *v = c->he_fused; return MFHE_OK;

@@ -75,6 +75,7 @@ struct mfhe_ctx {
     int64_t ntt_chunk_bytes = 192ll << 20;  // measured best at N = 2^15..2^17 (profiles/r01_ntt_sweep.txt)
     int ntt_plan = 0;
     int ntt_wg_per_cu = 16;  // NTT pass grid: workgroups per CU (0 = occupancy, 16 = one tile per WG; measured best)
+    int ntt_pack = 0;        // MFHE_OPT_NTT_PACK (measured slower, kept opt-in: DESIGN.md §3.1)
     int ntt_prefetch = 0;    // persistent NTT passes: prefetch the next tile's raw data (MFHE_OPT_NTT_PREFETCH)
     int num_cus = 256;
     int ntt_fused = 0;       // N = 2^15..2^17: both passes in one launch (MFHE_OPT_NTT_FUSED)

@@ -158,9 +158,26 @@ __device__ __forceinline__ TileLoc tile_loc(uint64_t* data, uint64_t batch, int 
 // One pass of the transform: LOG_G stages on groups of G = 2^LOG_G elements, one tile (NG groups) per
 // workgroup at a time.  Split into locate / load / compute+store so the persistent pass kernel can
 // prefetch and the fused kernel can run two different passes in one launch.
+// PACK (N = 2^16 two-pass plan, FP64 arithmetic, forward): the intermediate between the passes is stored as
+// 50-bit canonical residues instead of 64-bit words.  Unit (rb, t) = the 16 x 16 block of rows 16 rb.. and
+// columns 16 t.., column-major: LO[c][i] u32 (1024 B), MID[c][i] u16 (512 B), TOP[c] 16 x 2 bits (64 B),
+// padded to 13 cache lines (1664 B).  Unit (rb, t) lives in rows 16 rb .. 16 rb + 12 of column tile t: lines
+// the column pass of tile t read itself (it stages its 16 units in LDS and writes them, full lines only), and
+// that only the block pass of row block rb reads and then overwrites with its outputs, so no workgroup's
+// unread input is overwritten in either pass.  The block pass reads its 16 units with whole-line loads into
+// LDS, takes unit column (t, c) per thread from there and exchanges into its round-0 layout.  Intermediate traffic: 208 instead of 256 lines each way
+// (r02: the passes are fabric-bound, 25% fewer intermediate lines measured +11%, profiles/r02_pack.txt).
+constexpr int kPackUnitBytes = 1664;   // 13 lines
+constexpr int kPackRowBytes = 2048;    // one row of the 256 x 256 view of an N = 2^16 polynomial
+
 template <class A, class TS, int LOG_G, int LOG_R, int NG, bool COLS, bool INV, bool IN_RAW, bool OUT_RAW,
-          bool TWIST, bool BREV, bool UNI>
+          bool TWIST, bool BREV, bool UNI, bool PACK = false>
 struct NttPass {
+    static_assert(!PACK || (LOG_G == 8 && LOG_R == 4 && NG == 16 && UNI && !INV && !TWIST && !BREV &&
+                            (COLS ? (OUT_RAW && !IN_RAW) : (IN_RAW && !OUT_RAW))),
+                  "PACK: forward N = 2^16 two-pass plan only");
+    static constexpr bool PACK_OUT = PACK && COLS;   // column pass writes packed units
+    static constexpr bool PACK_IN = PACK && !COLS;   // block pass reads them
     using Gm = Geo<LOG_G, LOG_R>;
     using T = typename A::T;
     using Tw = typename A::Tw;
@@ -191,6 +208,24 @@ struct NttPass {
     static constexpr int kCpolSt = OUT_RAW ? MFHE_NTT_CPOL_MID_ST : MFHE_NTT_CPOL_OUT;
 
     __device__ __forceinline__ void load(const TileLoc& L, uint64_t (&raw)[R]) const {
+        if constexpr (PACK_IN) {
+            // the 16 units of this row block, 16 B chunks q = tid + NT s (1664 of them): every wave instruction
+            // reads 8 whole lines; compute_store sorts them out through LDS
+            const uint32_t rb = (uint32_t)(L.hi >> 4);
+            const char* base = (const char*)L.base + (size_t)(16 * rb) * kPackRowBytes;
+#pragma unroll
+            for (int s = 0; s < 7; ++s) {
+                const uint32_t q = threadIdx.x + NT * s;
+                ulonglong2 v = make_ulonglong2(0, 0);
+                if (s < 6 || q < 16 * kPackUnitBytes / 16) {
+                    const uint32_t t = q / 104, w = q - 104 * t;   // unit, chunk in the unit (8 per line)
+                    v = *(const ulonglong2*)(base + (w >> 3) * kPackRowBytes + t * 128 + (w & 7) * 16);
+                }
+                raw[2 * s] = v.x;
+                raw[2 * s + 1] = v.y;
+            }
+            return;
+        }
         if constexpr (UNI && kCpolLd != 0) {
             const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(L.base, 0, 0x7FFFFFFF, 0x00020000);
 #pragma unroll
@@ -199,7 +234,12 @@ struct NttPass {
                                                           rs, (int)(jidx(L, Gm::g_of(r_load, tau, k)) * 8u), 0, kCpolLd));
         } else {
 #pragma unroll
-            for (int k = 0; k < R; ++k) raw[k] = L.base[jidx(L, Gm::g_of(r_load, tau, k))];
+            for (int k = 0; k < R; ++k) {
+#ifdef MFHE_EXP_SKIP
+                if (IN_RAW && k >= 12) { raw[k] = 0; continue; }   // traffic experiment only (wrong results)
+#endif
+                raw[k] = L.base[jidx(L, Gm::g_of(r_load, tau, k))];
+            }
         }
     }
 
@@ -232,10 +272,49 @@ struct NttPass {
         const uint32_t tau_ = tau;
 
         T x[R];
+        if constexpr (PACK_IN) {
+            // staging image of the 16 units -> this thread's unit column (t, c) = rows 16 rb + i of column 16 t + c
+            __syncthreads();   // the previous tile's readers of this LDS are done
+            ulonglong2* img = (ulonglong2*)lds;
 #pragma unroll
-        for (int k = 0; k < R; ++k) {
-            x[k] = IN_RAW ? A::from_raw(raw[k]) : A::from_u64(raw[k]);
-            if constexpr (TWIST && !INV) x[k] = ar.mulmod(x[k], a.twist.get(twoff + jidx(L, Gm::g_of(r_load, tau_, k))));
+            for (int s = 0; s < 7; ++s) {
+                const uint32_t q = threadIdx.x + NT * s;
+                if (s < 6 || q < 16 * kPackUnitBytes / 16) img[q] = make_ulonglong2(raw[2 * s], raw[2 * s + 1]);
+            }
+            __syncthreads();
+            const uint32_t C = threadIdx.x, t = C >> 4, c = C & 15;
+            const char* ub = (const char*)lds + t * kPackUnitBytes;
+            uint64_t w[13];
+#pragma unroll
+            for (int s = 0; s < 4; ++s) {
+                const ulonglong2 v = *(const ulonglong2*)(ub + c * 64 + 16 * s);
+                w[2 * s] = v.x;
+                w[2 * s + 1] = v.y;
+            }
+#pragma unroll
+            for (int s = 0; s < 2; ++s) {
+                const ulonglong2 v = *(const ulonglong2*)(ub + 1024 + c * 32 + 16 * s);
+                w[8 + 2 * s] = v.x;
+                w[9 + 2 * s] = v.y;
+            }
+            w[12] = *(const uint32_t*)(ub + 1536 + c * 4);
+            __syncthreads();   // staging image consumed: the exchange may overwrite it
+#pragma unroll
+            for (int i = 0; i < 16; ++i) {
+                const uint64_t lo = (w[i >> 1] >> (32 * (i & 1))) & 0xFFFFFFFFull;
+                const uint64_t mid = (w[8 + (i >> 2)] >> (16 * (i & 3))) & 0xFFFFull;
+                const uint64_t top = (w[12] >> (2 * i)) & 3ull;
+                lds[(size_t)i * GS + Gm::pad(C)] = lo | (mid << 32) | (top << 48);
+            }
+            __syncthreads();
+#pragma unroll
+            for (int k = 0; k < R; ++k) x[k] = A::from_u64(my_lds[Gm::pad(Gm::g_of(0, tau_, k))]);
+        } else {
+#pragma unroll
+            for (int k = 0; k < R; ++k) {
+                x[k] = IN_RAW ? A::from_raw(raw[k]) : A::from_u64(raw[k]);
+                if constexpr (TWIST && !INV) x[k] = ar.mulmod(x[k], a.twist.get(twoff + jidx(L, Gm::g_of(r_load, tau_, k))));
+            }
         }
 
         auto exchange = [&](auto rf, auto rt, bool brev_pos) {
@@ -327,6 +406,38 @@ struct NttPass {
         // ---- store ----
         if constexpr (!INV && !COLS && (NR > 1 || BREV))
             exchange(std::integral_constant<int, NR - 1>{}, std::integral_constant<int, 0>{}, BREV);
+        if constexpr (PACK_OUT) {
+            // x[k]: row 16 tau + k of column off0 -> unit (rb = tau, t) column c = gl, staged in LDS
+            uint32_t lo[16], mid[8] = {}, top = 0;
+#pragma unroll
+            for (int k = 0; k < 16; ++k) {
+                const uint64_t u = ar.canon(x[k]);   // < q < 2^50
+                lo[k] = (uint32_t)u;
+                const uint32_t hi = (uint32_t)(u >> 32);
+                mid[k >> 1] |= (hi & 0xFFFFu) << (16 * (k & 1));
+                top |= (hi >> 16) << (2 * k);
+            }
+            __syncthreads();   // last exchange's readers are done with the LDS
+            char* ub = (char*)lds + tau_ * kPackUnitBytes;
+            uint4* plo = (uint4*)(ub + gl * 64);
+            uint4* pmid = (uint4*)(ub + 1024 + gl * 32);
+#pragma unroll
+            for (int s = 0; s < 4; ++s) plo[s] = make_uint4(lo[4 * s], lo[4 * s + 1], lo[4 * s + 2], lo[4 * s + 3]);
+#pragma unroll
+            for (int s = 0; s < 2; ++s) pmid[s] = make_uint4(mid[4 * s], mid[4 * s + 1], mid[4 * s + 2], mid[4 * s + 3]);
+            *(uint32_t*)(ub + 1536 + gl * 4) = top;
+            __syncthreads();
+            if (L.active) {
+                // line j of unit rb -> row 16 rb + j of this column tile (its own, already read lines)
+                const uint4* src = (const uint4*)lds;
+                char* dst = (char*)L.base + (size_t)(L.off0 & ~15u) * 8;
+                for (uint32_t q = threadIdx.x; q < 16 * kPackUnitBytes / 16; q += NT) {
+                    const uint32_t m = q >> 3, rb = m / 13, j = m - 13 * rb;
+                    *(uint4*)(dst + (size_t)(16 * rb + j) * kPackRowBytes + (q & 7) * 16) = src[q];
+                }
+            }
+            return;
+        }
         if (L.active) {
             if constexpr (UNI && kCpolSt != 0) {
                 const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(L.base, 0, 0x7FFFFFFF, 0x00020000);
@@ -345,6 +456,9 @@ struct NttPass {
                     const uint32_t g = Gm::g_of(r_store, tau_, k);
                     T y = x[k];
                     if constexpr (TWIST && INV) y = ar.mulmod(y, a.twist.get(twoff + jidx(L, g)));
+#ifdef MFHE_EXP_SKIP
+                    if (OUT_RAW && k >= 12) continue;   // traffic experiment only (wrong results)
+#endif
                     L.base[jidx(L, g)] = OUT_RAW ? A::to_raw(ar.reduce(y)) : ar.canon(y);
                 }
             }
@@ -399,11 +513,11 @@ constexpr int min_waves_per_simd(int nt) {
 }
 
 template <class A, class TS, int LOG_G, int LOG_R, int NG, bool COLS, bool INV, bool IN_RAW, bool OUT_RAW,
-          bool TWIST, bool BREV, bool UNI, bool PF>
+          bool TWIST, bool BREV, bool UNI, bool PF, bool PACK = false>
 __global__ __launch_bounds__(NG * (1 << (LOG_G - LOG_R)), min_waves_per_simd(NG * (1 << (LOG_G - LOG_R))))
 void ntt_pass_kernel(PassArgs<TS> a) {
     extern __shared__ __attribute__((aligned(16))) uint64_t lds[];
-    pass_loop<NttPass<A, TS, LOG_G, LOG_R, NG, COLS, INV, IN_RAW, OUT_RAW, TWIST, BREV, UNI>, PF>(a, lds);
+    pass_loop<NttPass<A, TS, LOG_G, LOG_R, NG, COLS, INV, IN_RAW, OUT_RAW, TWIST, BREV, UNI, PACK>, PF>(a, lds);
 }
 
 }  // namespace mfhe

@@ -31,12 +31,13 @@ struct NttJob {
     int plan;             // MFHE_OPT_NTT_PLAN
     int wg_per_cu;        // MFHE_OPT_NTT_WG_PER_CU (0 = occupancy limit)
     int prefetch;         // MFHE_OPT_NTT_PREFETCH
+    int pack = 0;         // MFHE_OPT_NTT_PACK: 50-bit packed intermediate (N = 2^16, F64)
     int num_cus;
     mfhe_ctx* ctx;        // owner of the fused sync buffer (null: raw phantom entry, no fused path)
 };
 
 template <class A, class TS, int LOG_G, int LOG_R, int NG, bool COLS, bool INV, bool IN_RAW, bool OUT_RAW, bool TWIST,
-          bool BREV, bool UNI>
+          bool BREV, bool UNI, bool PACK = false>
 static int launch_pass(const NttJob<TS>& j, int s0, hipStream_t st) {
     using Gm = Geo<LOG_G, LOG_R>;
     constexpr int TG = Gm::TG;
@@ -65,8 +66,8 @@ static int launch_pass(const NttJob<TS>& j, int s0, hipStream_t st) {
     a.nblocks = (uint32_t)nb;
     const bool need_lds = (Gm::NR > 1) || BREV;
     const size_t lds = need_lds ? (size_t)NG * Gm::GS * sizeof(uint64_t) : 0;
-    auto kern = j.prefetch ? ntt_pass_kernel<A, TS, LOG_G, LOG_R, NG, COLS, INV, IN_RAW, OUT_RAW, TWIST, BREV, UNI, true>
-                           : ntt_pass_kernel<A, TS, LOG_G, LOG_R, NG, COLS, INV, IN_RAW, OUT_RAW, TWIST, BREV, UNI, false>;
+    auto kern = j.prefetch ? ntt_pass_kernel<A, TS, LOG_G, LOG_R, NG, COLS, INV, IN_RAW, OUT_RAW, TWIST, BREV, UNI, true, PACK>
+                           : ntt_pass_kernel<A, TS, LOG_G, LOG_R, NG, COLS, INV, IN_RAW, OUT_RAW, TWIST, BREV, UNI, false, PACK>;
     // persistent grid: resident workgroups only (occupancy query cached per instantiation), a multiple of 8
     static int occ_cache[2] = {0, 0};
     int& occ = occ_cache[j.prefetch ? 1 : 0];
@@ -125,22 +126,46 @@ static int run_single(const NttJob<TS>& j, hipStream_t st) {
 // is still resident in the Infinity Cache (256 MiB) when pass B reads and overwrites it: HBM then
 // sees ~one read and one write per element instead of two of each.
 template <class A, class TS, int LOG_GA, int NGA, int LOG_GB, int NGB, bool INV>
+static int two_pass_chunk(const NttJob<TS>& c, int pass, hipStream_t st) {
+    // pass 0 = first pass of the direction (forward: column, inverse: block), 1 = second
+    constexpr bool kPackable = std::is_same<A, ArithF64>::value && LOG_GA == 8 && NGA == 16 && LOG_GB == 8 && NGB == 16;
+    if constexpr (!INV && kPackable) {
+        if (c.pack) {
+            if (pass == 0) return launch_pass<A, TS, LOG_GA, 4, NGA, true, false, false, true, false, false, true, true>(c, 0, st);
+            return launch_pass<A, TS, LOG_GB, 4, NGB, false, false, true, false, false, false, true, true>(c, LOG_GA, st);
+        }
+    }
+    if (!INV) {
+        if (pass == 0) return launch_pass<A, TS, LOG_GA, 4, NGA, true, false, false, true, false, false, true>(c, 0, st);
+        return launch_pass<A, TS, LOG_GB, 4, NGB, false, false, true, false, false, false, true>(c, LOG_GA, st);
+    }
+    if (pass == 0) return launch_pass<A, TS, LOG_GB, 4, NGB, false, true, false, true, false, false, true>(c, LOG_GA, st);
+    return launch_pass<A, TS, LOG_GA, 4, NGA, true, true, true, false, false, false, true>(c, 0, st);
+}
+
+// two-pass plans: pass A (COLS, s0 = 0, LOG_GA stages), pass B (block, s0 = LOG_GA).
+// The batch is processed in chunks of about chunk_bytes so the raw intermediate written by pass A
+// is still resident in the Infinity Cache (256 MiB) when pass B reads and overwrites it: HBM then
+// sees ~one read and one write per element instead of two of each.
+// (Running chunk c + 1's first pass on a second stream beside chunk c's second pass measured 13-23% slower
+// at 64-128 MiB chunks, r02 with sc1 nt output stores as in r01 without: DESIGN.md §3.1.)
+template <class A, class TS, int LOG_GA, int NGA, int LOG_GB, int NGB, bool INV>
 static int two_pass(const NttJob<TS>& j, hipStream_t st) {
     const uint64_t poly_bytes = (uint64_t)j.nl << (j.logN + 3);
     uint64_t cb = j.batch;
     if (j.chunk_bytes > 0) cb = std::max<uint64_t>(1, (uint64_t)j.chunk_bytes / poly_bytes);
-    for (uint64_t b0 = 0; b0 < j.batch; b0 += cb) {
+    const uint64_t nch = (j.batch + cb - 1) / cb;
+    auto chunk = [&](uint64_t k) {
         NttJob<TS> c = j;
+        const uint64_t b0 = k * cb;
         c.batch = std::min<uint64_t>(cb, j.batch - b0);
         c.data = j.data + b0 * ((uint64_t)j.nl << j.logN);
+        return c;
+    };
+    for (uint64_t k = 0; k < nch; ++k) {
         int rc;
-        if (!INV) {
-            if ((rc = launch_pass<A, TS, LOG_GA, 4, NGA, true, false, false, true, false, false, true>(c, 0, st))) return rc;
-            if ((rc = launch_pass<A, TS, LOG_GB, 4, NGB, false, false, true, false, false, false, true>(c, LOG_GA, st))) return rc;
-        } else {
-            if ((rc = launch_pass<A, TS, LOG_GB, 4, NGB, false, true, false, true, false, false, true>(c, LOG_GA, st))) return rc;
-            if ((rc = launch_pass<A, TS, LOG_GA, 4, NGA, true, true, true, false, false, false, true>(c, 0, st))) return rc;
-        }
+        if ((rc = two_pass_chunk<A, TS, LOG_GA, NGA, LOG_GB, NGB, INV>(chunk(k), 0, st))) return rc;
+        if ((rc = two_pass_chunk<A, TS, LOG_GA, NGA, LOG_GB, NGB, INV>(chunk(k), 1, st))) return rc;
     }
     return MFHE_OK;
 }

@@ -27,6 +27,7 @@ OPT_NTT_CHUNK_BYTES, OPT_NTT_PLAN, OPT_CRT_WORDS, OPT_NTT_WG_PER_CU, OPT_NTT_PRE
 OPT_NTT_FUSED, OPT_NTT_FUSED_LAG, OPT_NTT_FUSED_ERRORS, OPT_WCRT_MFMA = 6, 7, 8, 9
 OPT_CGEMM_MFMA, OPT_HE_FUSED, OPT_TRACE_SPLIT = 10, 11, 12
 XCHG_ALLGATHER, XCHG_ALLTOALL = 0, 1
+OPT_NTT_PACK = 13
 COMM_ID_BYTES = 128
 
 #: reference parameters (include/core/config.h:7-52)

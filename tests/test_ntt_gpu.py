@@ -264,3 +264,25 @@ def test_fused_two_pass_matches_oracle(mfhe, orc, log_n, batch, nl, lag):
         torch.cuda.synchronize()
         np.testing.assert_array_equal(mfhe.to_host_u64(d), data)
         assert ctx.get_option(mfhe.OPT_NTT_FUSED_ERRORS) == 0
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("batch,nl", [(3, 2), (17, 1)])
+def test_packed_intermediate_matches_oracle(mfhe, orc, batch, nl):
+    """MFHE_OPT_NTT_PACK (N = 2^16 forward two-pass, 50-bit packed intermediate units written over the column
+    tile's own lines): bit-exact vs the oracle and vs the unpacked plan, with chunking that splits the batch."""
+    import torch
+    N = 1 << 16
+    moduli = orc.gen_primes(50, 4 * N, nl)
+    ctx = mfhe.Context(moduli, 16)
+    data = rand_residues(np.random.default_rng(batch), batch, moduli, N)
+    want = orc.phantom_fwd(data, nl, 16, moduli)
+    for chunk in (0, 2 * nl * N * 8):
+        ctx.set_option(mfhe.OPT_NTT_CHUNK_BYTES, chunk)
+        ctx.set_option(mfhe.OPT_NTT_PACK, 1)
+        d = mfhe.to_device_u64(data)
+        ctx.ntt_fwd(d, batch=batch)
+        torch.cuda.synchronize()
+        np.testing.assert_array_equal(mfhe.to_host_u64(d), want)
+    ctx.set_option(mfhe.OPT_NTT_PACK, 0)
+    assert ctx.get_option(mfhe.OPT_NTT_PACK) == 0
