@@ -122,7 +122,7 @@ __global__ __launch_bounds__(P1::NT) void ntt_fused_kernel(FusedArgs<TS> f) {
                     const uint32_t g = k * Q + q;
                     const TileLoc L = p1.locate(g * K + u);
                     uint64_t raw[P1::R];
-                    p1.template load_pol<MFHE_FUSED_CPOL_IN>(L, raw);
+                    if constexpr (!P1::COL_DMA) p1.template load_pol<MFHE_FUSED_CPOL_IN>(L, raw);
                     flush(pend);   // the previous tile's stores drained behind this tile's loads
                     pend = k;
                     p1.compute_store(L, raw, lds);

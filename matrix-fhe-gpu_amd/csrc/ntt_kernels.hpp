@@ -40,6 +40,9 @@
 #ifndef MFHE_NTT_CPOL_MID_ST
 #define MFHE_NTT_CPOL_MID_ST 0
 #endif
+#ifndef MFHE_NTT_COL_DMA
+#define MFHE_NTT_COL_DMA 1   // forward column pass: tile -> LDS by LDS-DMA (16 B per lane), no VGPR staging
+#endif
 
 namespace mfhe {
 
@@ -176,6 +179,10 @@ struct NttPass {
     static_assert(!PACK || (LOG_G == 8 && LOG_R == 4 && NG == 16 && UNI && !INV && !TWIST && !BREV &&
                             (COLS ? (OUT_RAW && !IN_RAW) : (IN_RAW && !OUT_RAW))),
                   "PACK: forward N = 2^16 two-pass plan only");
+    // forward column pass reading the transform input: the 32 KiB tile goes global -> LDS by LDS-DMA
+    // (global_load_lds_dwordx4: 16 B per lane, each wave instruction 1 KiB), then round 0 reads it from LDS
+    static constexpr bool COL_DMA = MFHE_NTT_COL_DMA && COLS && !INV && !IN_RAW && UNI && !TWIST &&
+                                    (1 << LOG_G) * NG * 8 == 32768 && NG % 2 == 0;
     static constexpr bool PACK_OUT = PACK && COLS;   // column pass writes packed units
     static constexpr bool PACK_IN = PACK && !COLS;   // block pass reads them
     using Gm = Geo<LOG_G, LOG_R>;
@@ -208,6 +215,7 @@ struct NttPass {
     static constexpr int kCpolSt = OUT_RAW ? MFHE_NTT_CPOL_MID_ST : MFHE_NTT_CPOL_OUT;
 
     __device__ __forceinline__ void load(const TileLoc& L, uint64_t (&raw)[R]) const {
+        if constexpr (COL_DMA) return;   // compute_store issues the DMA once the LDS is free
         if constexpr (PACK_IN) {
             // the 16 units of this row block, 16 B chunks q = tid + NT s (1664 of them): every wave instruction
             // reads 8 whole lines; compute_store sorts them out through LDS
@@ -272,7 +280,25 @@ struct NttPass {
         const uint32_t tau_ = tau;
 
         T x[R];
-        if constexpr (PACK_IN) {
+        if constexpr (COL_DMA) {
+            typedef __attribute__((address_space(3))) void* lds_vp;
+            constexpr int CPR = NG / 2;                      // 16-B chunks per row of the tile
+            const uint32_t w = threadIdx.x >> 6, lane = threadIdx.x & 63;
+            const char* tile = (const char*)(L.base + (L.off0 - gl));   // row 0, first column of the tile
+            __syncthreads();   // the previous tile's readers of this LDS are done
+#pragma unroll
+            for (int i = 0; i < 32768 / (NT * 16); ++i) {
+                const uint32_t q = (i * (NT / 64) + w) * 64 + lane;   // chunk: row q / CPR, part q % CPR
+                const char* src = tile + (size_t)(q / CPR) * ((size_t)8 << (a.logN - LOG_G)) + (q % CPR) * 16;
+                __builtin_amdgcn_global_load_lds((const void*)src,
+                                                 (lds_vp)((char*)lds + (size_t)(i * (NT / 64) + w) * 1024), 16, 0,
+                                                 kCpolLd);
+            }
+            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+            __syncthreads();
+#pragma unroll
+            for (int k = 0; k < R; ++k) x[k] = A::from_u64(lds[(size_t)Gm::g_of(r_load, tau_, k) * NG + gl]);
+        } else if constexpr (PACK_IN) {
             // staging image of the 16 units -> this thread's unit column (t, c) = rows 16 rb + i of column 16 t + c
             __syncthreads();   // the previous tile's readers of this LDS are done
             ulonglong2* img = (ulonglong2*)lds;
