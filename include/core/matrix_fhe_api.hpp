@@ -199,6 +199,39 @@ class ResidueComm {
 void crt_recombine_sharded(ResidueComm& comm, const uint64_t* d_shard, double* d_out, int n2, int limbs, int lanes,
                            bool alltoall = false, hipStream_t stream = 0);
 
+// Residue-sharded HE pipeline (BASELINE C4): this rank's limbs [g*limbs_total/G, (g+1)*limbs_total/G) of
+// RNS_MODULI[0..limbs_total).  Keys, encoded messages and ciphertexts of a shard carry num_limbs =
+// limbs_total/G and are exactly those limbs of the unsharded ones (the uniform sampler of encrypt_pair is
+// seeded with the global limb index, HE.cu:564-578).  decrypt_and_decode runs the W-INTT on the shard, the
+// RCCL recombine of this rank's lanes (the per-lane compose loop of HE.cu:1653-1668), an all-gather of the
+// composed lanes and the W-DFT + XY-DFT: every rank receives the whole [BATCH_SIZE][n*n] message, identical
+// to decrypt_and_decode (HE.cu:1691-1708) of the unsharded ciphertexts.
+class ResidueShard {
+   public:
+    ResidueShard(ResidueComm& comm, int limbs_total);
+    ~ResidueShard();
+    ResidueShard(const ResidueShard&) = delete;
+    ResidueShard& operator=(const ResidueShard&) = delete;
+    int limb_base() const { return base_; }
+    int limbs() const { return lg_; }
+    int limbs_total() const { return total_; }
+    void generate_secret_key(SecretKey& sk) const;
+    void allocate_ciphertext(RLWECiphertext& ct) const;
+    // BatchedEncoder::encode_to_wntt_eval on the shard's limbs: d_msg [BATCH_SIZE][n*n] -> [BATCH_SIZE][limbs()][n*n]
+    void encode_to_wntt_eval(const hipDoubleComplex* d_msg_batch, uint64_t* d_out_re, uint64_t* d_out_im) const;
+    void encrypt_pair(const uint64_t* msg_re, const uint64_t* msg_im, const SecretKey& sk, RLWECiphertext& ct_re,
+                      RLWECiphertext& ct_im) const;
+    void decrypt_and_decode(const RLWECiphertext& ct_re, const RLWECiphertext& ct_im, const SecretKey& sk,
+                            hipDoubleComplex* output_msg, bool alltoall = false, hipStream_t stream = 0) const;
+    ::mfhe_ctx* context() const { return ctx_; }
+
+   private:
+    ResidueComm& comm_;
+    int total_ = 0, lg_ = 0, base_ = 0;
+    ::mfhe_ctx* ctx_ = nullptr;   // the shard's moduli, W-CRT tables, limb-shard sampler
+    ::mfhe_ctx* all_ = nullptr;   // all limbs_total moduli (CRT tables of the recombine), cached
+};
+
 // The C-ABI context (include/mfhe.h) behind this API for a given (n, limbs): moduli RNS_MODULI[0..limbs),
 // delta = SCALING_FACTOR, phantom + GL (+ W-CRT when with_wcrt) tables.  Built once, cached.
 struct mfhe_ctx* backend_context(int n, int limbs, bool with_wcrt = false);

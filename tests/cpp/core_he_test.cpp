@@ -181,6 +181,45 @@ int main() {
             err = std::max(err, std::hypot(ho[i].x - m1[i].x - m2[i].x, ho[i].y - m1[i].y - m2[i].y));
         std::printf("  max err %.3e\n", err);
         EXPECT(err < 1e-3, "homomorphic add err %.3e", err);
+
+        // residue-sharded pipeline through a 1-rank RCCL communicator: every stage equals the unsharded one
+        std::printf("[residue shard, 1-rank RCCL]\n");
+        {
+            ResidueComm comm(ResidueComm::unique_id(), 1, 0);
+            ResidueShard sh(comm, L);
+            EXPECT(sh.limb_base() == 0 && sh.limbs() == L && sh.limbs_total() == L, "shard geometry");
+            SecretKey ssk;
+            sh.generate_secret_key(ssk);
+            EXPECT(d2h(ssk.data, (size_t)PHI * L * n) == d2h(sk.data, (size_t)PHI * L * n), "shard keygen");
+            uint64_t *s1r = dev_alloc<uint64_t>(words), *s1i = dev_alloc<uint64_t>(words);
+            sh.encode_to_wntt_eval(dm1, s1r, s1i);
+            EXPECT(d2h(s1r, words) == d2h(e1r, words) && d2h(s1i, words) == d2h(e1i, words), "shard encode");
+            RLWECiphertext sr, si;
+            sh.allocate_ciphertext(sr);
+            sh.allocate_ciphertext(si);
+            sh.encrypt_pair(s1r, s1i, ssk, sr, si);
+            RLWECiphertext ur, ui;
+            allocate_ciphertext(ur, L);
+            allocate_ciphertext(ui, L);
+            encrypt_pair(e1r, e1i, sk, ur, ui);
+            EXPECT(d2h(sr.data, 2 * words) == d2h(ur.data, 2 * words), "shard encrypt_pair (re)");
+            EXPECT(d2h(si.data, 2 * words) == d2h(ui.data, 2 * words), "shard encrypt_pair (im)");
+            decrypt_and_decode(ur, ui, sk, dout);
+            const auto ref = d2h(dout, cnt);
+            hipDoubleComplex* dsh = dev_alloc<hipDoubleComplex>(cnt);
+            for (int a2a = 0; a2a < 2; ++a2a) {
+                sh.decrypt_and_decode(sr, si, ssk, dsh, a2a != 0);
+                const auto got = d2h(dsh, cnt);
+                size_t bad = 0;
+                for (size_t i = 0; i < cnt; ++i) bad += got[i].x != ref[i].x || got[i].y != ref[i].y;
+                EXPECT(bad == 0, "sharded decrypt_and_decode != unsharded (%zu values, alltoall %d)", bad, a2a);
+            }
+            bool threw = false;
+            try { ResidueShard bad_shard(comm, 0); } catch (const BackendError&) { threw = true; }
+            EXPECT(threw, "limbs_total 0 must throw");
+            for (auto* c : {&sr, &si, &ur, &ui}) free_ciphertext(*c);
+            hipFree(ssk.data); hipFree(s1r); hipFree(s1i); hipFree(dsh);
+        }
         for (auto* c : {&c1r, &c1i, &c2r, &c2i}) free_ciphertext(*c);
         hipFree(sk.data); hipFree(dm1); hipFree(dm2); hipFree(dout);
         hipFree(e1r); hipFree(e1i); hipFree(e2r); hipFree(e2i);
