@@ -85,6 +85,41 @@ def test_crt_compose_and_f64_match_oracle(mfhe, orc):
         np.testing.assert_array_equal(f2.cpu().numpy()[::2], ref, err_msg=name)
 
 
+@pytest.mark.parametrize("nc", [4096, 3001])
+def test_vector_and_scalar_kernels_agree(mfhe, orc, nc):
+    """Even ncoeff with unit stride and 16-B aligned buffers runs the two-coefficient decompose kernel (16-B
+    loads/stores), odd ncoeff or a misaligned output the one-coefficient kernel: both bit-exact against the
+    oracle.  The compose then mixes fast and slow paths in one launch (random residues fail the fast-path
+    check, small values take it), at unit and non-unit output strides."""
+    import torch
+    rng = np.random.default_rng(nc)
+    for moduli, log_n in ((orc.gen_primes(50, 1 << 18, 8), 16), (orc.gen_primes(50, 1 << 18, 16), 16), (RNS, 6)):
+        ctx = mfhe.Context(moduli, log_n)
+        L, npoly = len(moduli), 3
+        z = _values(rng, npoly * nc, ctx.delta)
+        z[1::7] = rng.uniform(-1e6, 1e6, z[1::7].size)
+        zt = torch.from_numpy(z).cuda()
+        expect_r = orc.rns_decompose(z, npoly, nc, moduli, ctx.delta)
+        for off in (0, 1):   # off = 1: an 8-B aligned (not 16-B) output view
+            buf = torch.zeros(npoly * L * nc + 1, dtype=torch.int64, device="cuda")
+            r = buf[off:off + npoly * L * nc]
+            ctx.rns_decompose(zt, r, npoly, nc)
+            torch.cuda.synchronize()
+            np.testing.assert_array_equal(mfhe.to_host_u64(r), expect_r)
+        q = np.array(moduli, np.uint64)[None, :, None]
+        res = expect_r.reshape(npoly, L, nc).copy()
+        res[2] = rng.integers(0, 2 ** 63, (L, nc), dtype=np.uint64) % q[0]   # slow path
+        res = res.ravel()
+        omag, oneg = orc.crt_compose(res, npoly, L, nc, moduli, ctx.crt_words)
+        ref = orc.big_to_f64(omag, oneg, ctx.crt_words, ctx.delta)
+        d = mfhe.to_device_u64(res)
+        for stride in (1, 3):
+            f = torch.zeros(npoly * nc * stride, dtype=torch.float64, device="cuda")
+            ctx.crt_compose_f64(d, f, npoly, nc, out_stride=stride)
+            torch.cuda.synchronize()
+            np.testing.assert_array_equal(f.cpu().numpy()[::stride], ref)
+
+
 def test_decompose_compose_roundtrip_full_size(mfhe):
     """Size-independent property at C3 scale: compose_f64(decompose(z)) == round(z*delta)/delta."""
     import torch

@@ -103,6 +103,47 @@ def test_extreme_moduli_and_values(mfhe, orc):
             np.testing.assert_array_equal(mfhe.to_host_u64(d), data)
 
 
+def test_extreme_moduli_and_values_u64(mfhe, orc):
+    """U64 path edge: the largest primes below 2^62 (the Harvey 4q < 2^64 limit) with all-(q-1), all-zero
+    and alternating inputs, single-pass and two-pass sizes."""
+    import torch
+    for log_n in (6, 14, 16, 17):
+        N = 1 << log_n
+        moduli = orc.gen_primes(62, 2 * N, 2)
+        assert all(2 ** 61 < q < 2 ** 62 for q in moduli)
+        ctx = mfhe.Context(moduli, log_n)
+        assert ctx.info().arith == mfhe.ARITH_U64
+        q = np.array(moduli, np.uint64)[None, :, None]
+        for fill in ("max", "zero", "alt"):
+            if fill == "max":
+                data = np.broadcast_to(q - 1, (2, 2, N)).copy().ravel()
+            elif fill == "zero":
+                data = np.zeros(2 * 2 * N, np.uint64)
+            else:
+                data = np.where(np.arange(N)[None, None, :] % 2 == 0, q - 1, 0).astype(np.uint64)
+                data = np.broadcast_to(data, (2, 2, N)).copy().ravel()
+            d = mfhe.to_device_u64(data)
+            ctx.ntt_fwd(d)
+            torch.cuda.synchronize()
+            np.testing.assert_array_equal(mfhe.to_host_u64(d), orc.phantom_fwd(data, 2, log_n, moduli))
+            ctx.ntt_inv(d)
+            torch.cuda.synchronize()
+            np.testing.assert_array_equal(mfhe.to_host_u64(d), data)
+
+
+def test_empty_batch_is_a_no_op(mfhe, orc):
+    """batch 0 (an empty ragged tail) launches nothing and touches nothing, on every plan."""
+    import torch
+    for log_n in (6, 14, 16):
+        moduli = orc.gen_primes(50, 4 << log_n, 2)
+        ctx = mfhe.Context(moduli, log_n)
+        sentinel = torch.full((16,), 7, dtype=torch.int64, device="cuda")
+        ctx.ntt_fwd(sentinel, batch=0)
+        ctx.ntt_inv(sentinel, batch=0)
+        torch.cuda.synchronize()
+        assert bool((sentinel == 7).all())
+
+
 def test_limb_subrange(mfhe, orc):
     """start_limb / nlimbs select moduli start..start+nl-1 (the fnwt_1d start_modulus_idx)."""
     import torch
