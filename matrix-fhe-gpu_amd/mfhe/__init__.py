@@ -383,8 +383,26 @@ class Context:
         fn = getattr(lib, name)
         check(fn(self._h, *ptrs, _stream_ptr(stream)), name)
 
-    def wcrt_fwd(self, src, dst, stream=None): self._call("mfhe_wcrt_fwd", _ptr(src), _ptr(dst), stream=stream); return dst
-    def wcrt_inv(self, src, dst, stream=None): self._call("mfhe_wcrt_inv", _ptr(src), _ptr(dst), stream=stream); return dst
+    # host-side sizes of the fixed-geometry buffers (phi = 512 W-lanes), checked before raw pointers cross
+    def _mat(self):   # one matrix-major [phi][L][n*n] (or poly-major [phi*n][L][n]) residue array
+        return 512 * self.L * self.N * self.N
+
+    def _msg(self):   # one [phi][n*n] complex message, interleaved doubles
+        return 2 * 512 * self.N * self.N
+
+    def _sk(self):    # secret key [phi][L][n]
+        return 512 * self.L * self.N
+
+    def _sizes(self, what, *pairs):
+        for t, words in pairs:
+            _need(t, words, what)
+
+    def wcrt_fwd(self, src, dst, stream=None):
+        self._sizes("wcrt_fwd", (src, self._mat()), (dst, self._mat()))
+        self._call("mfhe_wcrt_fwd", _ptr(src), _ptr(dst), stream=stream); return dst
+    def wcrt_inv(self, src, dst, stream=None):
+        self._sizes("wcrt_inv", (src, self._mat()), (dst, self._mat()))
+        self._call("mfhe_wcrt_inv", _ptr(src), _ptr(dst), stream=stream); return dst
     def wcrt_fwd_vector(self, src, dst, stream=None):
         self._call("mfhe_wcrt_fwd_vector", _ptr(src), _ptr(dst), stream=stream); return dst
     def wcrt_fwd_centered(self, src, dst, stream=None):
@@ -398,8 +416,11 @@ class Context:
     def wdft_inv_pair(self, re, im, out_re, out_im, stream=None):
         self._call("mfhe_wdft_inv_pair", _ptr(re), _ptr(im), _ptr(out_re), _ptr(out_im), stream=stream)
     def ct_add(self, ct1, ct2, res, stream=None):
+        self._sizes("ct_add", *[(t, 2 * self._mat()) for t in (ct1, ct2, res)])
         self._call("mfhe_ct_add", _ptr(ct1), _ptr(ct2), _ptr(res), stream=stream); return res
     def ct_mul_tensor(self, ct1, ct2, d0, d1, d2, stream=None):
+        self._sizes("ct_mul_tensor", (ct1, 2 * self._mat()), (ct2, 2 * self._mat()),
+                    *[(t, self._mat()) for t in (d0, d1, d2)])
         self._call("mfhe_ct_mul_tensor", _ptr(ct1), _ptr(ct2), _ptr(d0), _ptr(d1), _ptr(d2), stream=stream)
     # ---- trace GEMM, planes [batch][nlimbs][n][n] (batched_trace.cu) ----
     @staticmethod
@@ -435,21 +456,34 @@ class Context:
     def xy_idft(self, src, dst, lanes, stream=None):
         check(lib.mfhe_xy_idft(self._h, _ptr(src), _ptr(dst), lanes, _stream_ptr(stream)), "xy_idft"); return dst
     def matrix_to_poly(self, src, dst, stream=None):
+        self._sizes("matrix_to_poly", (src, self._mat()), (dst, self._mat()))
         self._call("mfhe_matrix_to_poly", _ptr(src), _ptr(dst), stream=stream); return dst
     def poly_to_matrix(self, src, dst, stream=None):
+        self._sizes("poly_to_matrix", (src, self._mat()), (dst, self._mat()))
         self._call("mfhe_poly_to_matrix", _ptr(src), _ptr(dst), stream=stream); return dst
     def reserve_workspace(self): check(lib.mfhe_ctx_reserve_workspace(self._h), "reserve_workspace")
     def encode(self, msg, out_re, out_im, stream=None):
+        self._sizes("encode", (msg, self._msg()), (out_re, self._mat()), (out_im, self._mat()))
         self._call("mfhe_encode", _ptr(msg), _ptr(out_re), _ptr(out_im), stream=stream)
     def decode(self, ev_re, ev_im, msg, stream=None):
+        self._sizes("decode", (ev_re, self._mat()), (ev_im, self._mat()), (msg, self._msg()))
         self._call("mfhe_decode", _ptr(ev_re), _ptr(ev_im), _ptr(msg), stream=stream); return msg
-    def keygen(self, sk, stream=None): self._call("mfhe_keygen", _ptr(sk), stream=stream); return sk
-    def encrypt(self, m, sk, ct, stream=None): self._call("mfhe_encrypt", _ptr(m), _ptr(sk), _ptr(ct), stream=stream)
+    def keygen(self, sk, stream=None):
+        self._sizes("keygen", (sk, self._sk()))
+        self._call("mfhe_keygen", _ptr(sk), stream=stream); return sk
+    def encrypt(self, m, sk, ct, stream=None):
+        self._sizes("encrypt", (m, self._mat()), (sk, self._sk()), (ct, 2 * self._mat()))
+        self._call("mfhe_encrypt", _ptr(m), _ptr(sk), _ptr(ct), stream=stream)
     def encrypt_pair(self, m_re, m_im, sk, ct_re, ct_im, stream=None):
+        self._sizes("encrypt_pair", (m_re, self._mat()), (m_im, self._mat()), (sk, self._sk()),
+                    (ct_re, 2 * self._mat()), (ct_im, 2 * self._mat()))
         self._call("mfhe_encrypt_pair", _ptr(m_re), _ptr(m_im), _ptr(sk), _ptr(ct_re), _ptr(ct_im), stream=stream)
     def decrypt_to_eval(self, ct, sk, out, stream=None):
+        self._sizes("decrypt_to_eval", (ct, 2 * self._mat()), (sk, self._sk()), (out, self._mat()))
         self._call("mfhe_decrypt_to_eval", _ptr(ct), _ptr(sk), _ptr(out), stream=stream); return out
     def decrypt_and_decode(self, ct_re, ct_im, sk, msg, stream=None):
+        self._sizes("decrypt_and_decode", (ct_re, 2 * self._mat()), (ct_im, 2 * self._mat()), (sk, self._sk()),
+                    (msg, self._msg()))
         self._call("mfhe_decrypt_and_decode", _ptr(ct_re), _ptr(ct_im), _ptr(sk), _ptr(msg), stream=stream); return msg
 
     # ---- residue sharding across GPUs (BASELINE C4, include/mfhe.h) ----
@@ -459,12 +493,15 @@ class Context:
 
     def decode_sharded(self, ctx_all: "Context", comm: "Comm", mode, ev_re, ev_im, msg, stream=None):
         m = _XCHG[mode] if isinstance(mode, str) else mode
+        self._sizes("decode_sharded", (ev_re, self._mat()), (ev_im, self._mat()), (msg, self._msg()))
         check(lib.mfhe_decode_sharded(self._h, ctx_all._h, comm._h, m, _ptr(ev_re), _ptr(ev_im), _ptr(msg),
                                       _stream_ptr(stream)), "decode_sharded")
         return msg
 
     def decrypt_and_decode_sharded(self, ctx_all: "Context", comm: "Comm", mode, ct_re, ct_im, sk, msg, stream=None):
         m = _XCHG[mode] if isinstance(mode, str) else mode
+        self._sizes("decrypt_and_decode_sharded", (ct_re, 2 * self._mat()), (ct_im, 2 * self._mat()),
+                    (sk, self._sk()), (msg, self._msg()))
         check(lib.mfhe_decrypt_and_decode_sharded(self._h, ctx_all._h, comm._h, m, _ptr(ct_re), _ptr(ct_im), _ptr(sk),
                                                   _ptr(msg), _stream_ptr(stream)), "decrypt_and_decode_sharded")
         return msg

@@ -502,3 +502,54 @@ def test_wcrt_mfma_matches_valu_and_oracle(mfhe, orc, n, L):
         ref = np.zeros_like(x)
         orc.L.orc_wntt_forward_matrix(P(x), P(ref), n, L, 512, P(U64(RNS[:L])), orc.L.orc_he_V(h.h))
         np.testing.assert_array_equal(outs[1][0], ref)
+
+
+@pytest.mark.parametrize("n,log_n,L", [(8, 3, 11), (64, 6, 11), (16, 4, 3)])
+def test_layout_transforms_vs_oracle(mfhe, orc, n, log_n, L):
+    """matrix_to_poly_kernel / poly_to_matrix_kernel (HE.cu:1330-1368): matrix-major [phi][L][n*n] <->
+    poly-major [phi*n][L][n], standalone, bit-exact against the oracle in both directions, and a round trip."""
+    import torch
+    ctx = mfhe.Context(RNS[:L], log_n, CONV)
+    x = _rand_mat(np.random.default_rng(n + L), n, L)
+    ref = np.empty_like(x)
+    orc.L.orc_matrix_to_poly(P(x), P(ref), n, L, 512)
+    got = torch.empty(x.size, dtype=torch.int64, device="cuda")
+    ctx.matrix_to_poly(_dev(mfhe, x), got)
+    torch.cuda.synchronize()
+    np.testing.assert_array_equal(mfhe.to_host_u64(got), ref)
+    back_ref = np.empty_like(x)
+    orc.L.orc_poly_to_matrix(P(ref), P(back_ref), n, L, 512)
+    np.testing.assert_array_equal(back_ref, x)
+    back = torch.empty_like(got)
+    ctx.poly_to_matrix(got, back)
+    torch.cuda.synchronize()
+    np.testing.assert_array_equal(mfhe.to_host_u64(back), x)
+
+
+def test_he_wrappers_reject_undersized_buffers(mfhe, small):
+    """The Python layer checks every fixed-geometry buffer (phi = 512 lanes) before a raw pointer crosses the
+    C ABI: an undersized tensor is a ValueError on the host, never an out-of-bounds device access."""
+    import torch
+    n, ctx, _ = small
+    W = 512 * 11 * n * n
+    big = torch.zeros(2 * W, dtype=torch.int64, device="cuda")
+    short = torch.zeros(W - 1, dtype=torch.int64, device="cuda")
+    msg = torch.zeros(2 * 512 * n * n, dtype=torch.float64, device="cuda")
+    sk = torch.zeros(512 * 11 * n, dtype=torch.int64, device="cuda")
+    with pytest.raises(ValueError):
+        ctx.matrix_to_poly(short, big)
+    with pytest.raises(ValueError):
+        ctx.wcrt_fwd(big, short)
+    with pytest.raises(ValueError):
+        ctx.encode(msg[:-1], big, big)
+    with pytest.raises(ValueError):
+        ctx.keygen(sk[:-1])
+    with pytest.raises(ValueError):
+        ctx.encrypt_pair(big, big, sk, big, short)
+    with pytest.raises(ValueError):
+        ctx.decrypt_and_decode(big, big[:W], sk, msg)
+    with pytest.raises(ValueError):
+        ctx.ct_add(big, big, short)
+    # the exact sizes pass
+    ctx.matrix_to_poly(big[:W], big[W:])
+    torch.cuda.synchronize()
