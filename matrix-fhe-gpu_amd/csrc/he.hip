@@ -34,8 +34,8 @@ __global__ void layout_kernel(const uint64_t* __restrict__ in, uint64_t* __restr
     if (i >= total) return;
     const uint64_t n = 1ull << log_n, n2 = n * n;
     const uint64_t x = i & (n - 1), y = (i >> log_n) & (n - 1);
-    const uint64_t wl = i >> (2 * log_n), l = wl % L, w = wl / L;
-    const uint64_t p = ((w * n + y) * L + l) * n + x;
+    const uint32_t wl = (uint32_t)(i >> (2 * log_n)), w = wl / (uint32_t)L, l = wl - w * (uint32_t)L;   // wl < 2^32
+    const uint64_t p = (((uint64_t)w * n + y) * L + l) * n + x;
     (void)n2;
     if (TO_POLY) out[p] = in[i];
     else out[i] = in[p];
@@ -62,12 +62,16 @@ __global__ void ternary_kernel(uint64_t* s, const uint64_t* qmu, int L, int log_
 __global__ void uniform_kernel(uint64_t* a, const uint64_t* qmu, int L, int log_n, uint64_t total, int lbase, int Ltot) {
     const uint64_t idx = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x;
     if (idx >= total) return;
-    const uint64_t n2 = 1ull << (2 * log_n), pos = idx & (n2 - 1), wl = idx >> (2 * log_n);
-    const uint64_t w = wl / (uint64_t)L;
-    const int limb = (int)(wl - w * (uint64_t)L);
-    uint64_t seed = 123456789ULL + ((w * (uint64_t)Ltot + (uint64_t)(lbase + limb)) << (2 * log_n)) + pos;
+    const uint64_t n2 = 1ull << (2 * log_n), pos = idx & (n2 - 1);
+    const uint32_t wl = (uint32_t)(idx >> (2 * log_n)), w = wl / (uint32_t)L;   // wl < 2^32: 32-bit division
+    const int limb = (int)(wl - w * (uint32_t)L);
+    uint64_t seed = 123456789ULL + (((uint64_t)w * (uint64_t)Ltot + (uint64_t)(lbase + limb)) << (2 * log_n)) + pos;
     seed = seed * 6364136223846793005ULL + 1442695040888963407ULL;
-    a[idx] = seed % qmu[2 * limb];
+    // seed % q by Barrett (mu = floor(2^64 / q)): the quotient estimate is at most 2 low, so r < 3q
+    const uint64_t q = qmu[2 * limb], mu = qmu[2 * limb + 1];
+    uint64_t r = seed - __umul64hi(seed, mu) * q;
+    r = r >= q ? r - q : r;
+    a[idx] = r >= q ? r - q : r;
 }
 
 __device__ __forceinline__ uint64_t splitmix64(uint64_t x) {
@@ -145,8 +149,8 @@ __global__ __launch_bounds__(256) void enc_combine_kernel(const uint64_t* __rest
     if (i >= total) return;
     const uint64_t n = 1ull << log_n;
     const uint64_t x = i & (n - 1), y = (i >> log_n) & (n - 1);
-    const uint64_t wl = i >> (2 * log_n), l = wl % L, w = wl / L;
-    const uint64_t p = ((w * n + y) * L + l) * n + x;
+    const uint32_t wl = (uint32_t)(i >> (2 * log_n)), w = wl / (uint32_t)L, l = wl - w * (uint32_t)L;   // wl < 2^32
+    const uint64_t p = (((uint64_t)w * n + y) * L + l) * n + x;
     const uint64_t q = qmu[2 * l];
     const uint64_t tv = t[p], ev = e[p], av = aev[p];
     auto bval = [&](uint64_t m) {
@@ -291,14 +295,15 @@ __global__ __launch_bounds__(256) void enc_ring_kernel(RingArgs ra, const uint64
     const uint64_t R = g / T;
     const bool live = R < ra.rows;                     // dead lanes still take part in the shuffles
     const uint64_t Rc = live ? R : 0;
-    const uint64_t y = Rc % N, wl = Rc / N, l = wl % ra.L, w = wl / ra.L;
+    const uint64_t y = Rc % N;
+    const uint32_t wl = (uint32_t)(Rc / N), w = wl / (uint32_t)ra.L, l = wl - w * (uint32_t)ra.L;   // wl < 2^32
     const uint64_t i0 = Rc * N + 4 * j;                                  // matrix-major
-    const uint64_t p0 = ((w * N + y) * ra.L + l) * N + 4 * j;            // poly-major
+    const uint64_t p0 = (((uint64_t)w * N + y) * ra.L + l) * N + 4 * j;  // poly-major
     const LimbConst lc = ra.lf[l];
     const ArithF64 ar(lc);
     uint64_t av[4], sk[4];
     ld4(aev + p0, av);
-    ld4(ra.sk + (w * ra.L + l) * N + 4 * j, sk);
+    ld4(ra.sk + ((uint64_t)w * ra.L + l) * N + 4 * j, sk);
     double x[4], sv[4];
 #pragma unroll
     for (int s = 0; s < 4; ++s) {
@@ -341,14 +346,15 @@ __global__ __launch_bounds__(256) void dec_ring_kernel(RingArgs ra, const uint64
     const uint64_t R = g / T;
     const bool live = R < ra.rows;
     const uint64_t Rc = live ? R : 0;
-    const uint64_t y = Rc % N, wl = Rc / N, l = wl % ra.L, w = wl / ra.L;
+    const uint64_t y = Rc % N;
+    const uint32_t wl = (uint32_t)(Rc / N), w = wl / (uint32_t)ra.L, l = wl - w * (uint32_t)ra.L;   // wl < 2^32
     const uint64_t i0 = Rc * N + 4 * j, total = ra.rows * N;
-    const uint64_t p0 = ((w * N + y) * ra.L + l) * N + 4 * j;
+    const uint64_t p0 = (((uint64_t)w * N + y) * ra.L + l) * N + 4 * j;
     const LimbConst lc = ra.lf[l];
     const ArithF64 ar(lc);
     uint64_t av[4], sk[4];
     ld4(ct + total + i0, av);
-    ld4(ra.sk + (w * ra.L + l) * N + 4 * j, sk);
+    ld4(ra.sk + ((uint64_t)w * ra.L + l) * N + 4 * j, sk);
     double x[4], sv[4];
 #pragma unroll
     for (int s = 0; s < 4; ++s) {
