@@ -21,14 +21,29 @@ namespace mfhe {
 
 using u128 = unsigned __int128;
 
+// (poly, coefficient) of a flat index: a shift for power-of-two ncoeff (lg >= 0), else a 64-bit division
+__device__ __forceinline__ void split_index(uint64_t i, uint64_t n, int lg, uint64_t& p, uint64_t& c) {
+    if (lg >= 0) {
+        p = i >> lg;
+        c = i & (n - 1);
+    } else {
+        p = i / n;
+        c = i - p * n;
+    }
+}
+static inline int log2_or_neg(uint64_t n) {
+    return (n && !(n & (n - 1))) ? __builtin_ctzll(n) : -1;
+}
+
 // ---------------- RNS decompose ----------------
 __global__ __launch_bounds__(256) void rns_decompose_kernel(const double* __restrict__ in, uint64_t in_stride,
-                                                            uint64_t total, uint64_t ncoeff, int L,
+                                                            uint64_t total, uint64_t ncoeff, int lg, int L,
                                                             const uint64_t* __restrict__ qmu, double delta,
                                                             uint64_t* __restrict__ out) {
     const uint64_t i = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x;
     if (i >= total) return;
-    const uint64_t p = i / ncoeff, c = i - p * ncoeff;
+    uint64_t p, c;
+    split_index(i, ncoeff, lg, p, c);
     const double z = in[i * in_stride] * delta;
     const long long x = llround(z);
     const bool neg = x < 0;
@@ -46,12 +61,13 @@ __global__ __launch_bounds__(256) void rns_decompose_kernel(const double* __rest
 // Two coefficients per thread (ncoeff even, unit input stride, 16-B aligned buffers): one 16-B load and L
 // 16-B stores per thread instead of one and L 8-B ones -- half the memory instructions for the same bytes.
 __global__ __launch_bounds__(256) void rns_decompose_x2_kernel(const double2* __restrict__ in, uint64_t total2,
-                                                               uint64_t ncoeff2, int L,
+                                                               uint64_t ncoeff2, int lg2, int L,
                                                                const uint64_t* __restrict__ qmu, double delta,
                                                                ulonglong2* __restrict__ out) {
     const uint64_t i = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x;
     if (i >= total2) return;
-    const uint64_t p = i / ncoeff2, c = i - p * ncoeff2;
+    uint64_t p, c;
+    split_index(i, ncoeff2, lg2, p, c);
     const double2 z = in[i];
     const long long x0 = llround(z.x * delta), x1 = llround(z.y * delta);
     const bool n0 = x0 < 0, n1 = x1 < 0;
@@ -340,6 +356,7 @@ struct CrtArgs {
     const uint64_t *M, *Q, *Qh;
     const CrtLimbF* lf;       // FP64 fast-path constants (null: integer fast path)
     bool qbig;                // Q_half >= 2^64: every |c| < 2^62 is inside (-Q/2, Q/2)
+    int lg_nc;                // log2(ncoeff), or -1 when ncoeff is not a power of two
 };
 
 template <int W>
@@ -347,7 +364,8 @@ __global__ __launch_bounds__(256) void crt_compose_kernel(CrtArgs a, uint64_t* _
                                                           uint8_t* __restrict__ out_neg) {
     const uint64_t i = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x;
     if (i >= a.total) return;
-    const uint64_t p = i / a.ncoeff, c = i - p * a.ncoeff;
+    uint64_t p, c;
+    split_index(i, a.ncoeff, a.lg_nc, p, c);
     uint64_t mag[W];
     bool neg;
     compose_one<W>(a.in + p * (uint64_t)a.Lg * a.ncoeff + c, a.ncoeff, a.L, a.Lg, a.shard_stride, a.qmu, a.inv,
@@ -363,7 +381,8 @@ __global__ __launch_bounds__(256) void crt_compose_f64_kernel(CrtArgs a, double 
                                                               uint64_t out_stride) {
     const uint64_t i = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x;
     if (i >= a.total) return;
-    const uint64_t p = i / a.ncoeff, c = i - p * a.ncoeff;
+    uint64_t p, c;
+    split_index(i, a.ncoeff, a.lg_nc, p, c);
     uint64_t mag[W];
     bool neg;
     compose_one<W>(a.in + p * (uint64_t)a.Lg * a.ncoeff + c, a.ncoeff, a.L, a.Lg, a.shard_stride, a.qmu, a.inv,
@@ -392,6 +411,7 @@ static CrtArgs crt_args(const mfhe_ctx* c, const uint64_t* in, uint64_t npoly, u
     a.in = in;
     a.ncoeff = ncoeff;
     a.total = npoly * ncoeff;
+    a.lg_nc = log2_or_neg(ncoeff);
     a.L = c->L;
     a.Lg = c->L;
     a.shard_stride = 0;
@@ -420,11 +440,12 @@ extern "C" int mfhe_rns_decompose(mfhe_ctx* c, const double* in, size_t in_strid
     if (!in || !out || in_stride == 0) return set_error(MFHE_EINVAL, "mfhe_rns_decompose: bad pointer/stride");
     if (in_stride == 1 && ncoeff % 2 == 0 && ((uintptr_t)in & 15) == 0 && ((uintptr_t)out & 15) == 0)
         hipLaunchKernelGGL(rns_decompose_x2_kernel, grid1d(total / 2, 256), dim3(256), 0, (hipStream_t)s,
-                           (const double2*)in, total / 2, (uint64_t)ncoeff / 2, c->L, c->d_rns_mu, c->delta,
-                           (ulonglong2*)out);
+                           (const double2*)in, total / 2, (uint64_t)ncoeff / 2, log2_or_neg(ncoeff / 2), c->L,
+                           c->d_rns_mu, c->delta, (ulonglong2*)out);
     else
         hipLaunchKernelGGL(rns_decompose_kernel, grid1d(total, 256), dim3(256), 0, (hipStream_t)s, in,
-                           (uint64_t)in_stride, total, (uint64_t)ncoeff, c->L, c->d_rns_mu, c->delta, out);
+                           (uint64_t)in_stride, total, (uint64_t)ncoeff, log2_or_neg(ncoeff), c->L, c->d_rns_mu,
+                           c->delta, out);
     MFHE_CHECK_LAUNCH("rns_decompose_kernel");
     return MFHE_OK;
 }
