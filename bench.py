@@ -599,7 +599,7 @@ def main():
             out["ms_per_step"] = step_s * 1e3
             alg_bytes = 16.0 * N * batch * L       # 8N read + 8N write per NTT
             ach = alg_bytes / (res["fwd_ev_ms"] * 1e-3) / 1e9
-            chunk_polys = max(1, (192 << 20) // (L * N * 8))
+            chunk_polys = max(1, ctx.get_option(mfhe.OPT_NTT_CHUNK_BYTES) // (L * N * 8))
             nchunks = -(-batch // chunk_polys) if log_n > 14 else 1
             kname = (f"mfhe_ntt_fwd call = {nchunks} chunks x (column pass + block pass) ntt_pass_kernel launches"
                      if log_n > 14 else "mfhe_ntt_fwd call = 1 single-pass ntt_pass_kernel launch")

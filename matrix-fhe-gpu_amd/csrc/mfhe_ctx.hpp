@@ -72,7 +72,7 @@ struct mfhe_ctx {
     double delta = 0.0;
     int device = 0;
     std::vector<uint64_t> moduli;
-    int64_t ntt_chunk_bytes = 192ll << 20;  // measured best at N = 2^15..2^17 (profiles/r01_ntt_sweep.txt)
+    int64_t ntt_chunk_bytes = 240ll << 20;  // measured best at N = 2^15..2^17 (profiles/r02_chunk.txt)
     int ntt_plan = 0;
     int ntt_wg_per_cu = 16;  // NTT pass grid: workgroups per CU (0 = occupancy, 16 = one tile per WG; measured best)
     int ntt_pack = 0;        // MFHE_OPT_NTT_PACK (measured slower, kept opt-in: DESIGN.md §3.1)
