@@ -270,7 +270,12 @@ static int run_phantom(const NttJob<TS>& j, hipStream_t st) {
         case 14: return two_pass<A, TS, 7, 32, 7, 32, INV>(j, st);
         case 15: return two_pass<A, TS, 8, 16, 7, 32, INV>(j, st);
         case 16: return two_pass<A, TS, 8, 16, 8, 16, INV>(j, st);
-        case 17: return two_pass<A, TS, 9, 8, 8, 16, INV>(j, st);
+        // N = 2^17: the forward column pass takes 8 stages on 16-column tiles (128-B row segments) and the block
+        // pass 9; the inverse keeps 9 column + 8 block stages.  Measured per direction (profiles/r02_n17_split.txt):
+        // forward +5%, inverse -2.5% with the other split.
+        case 17:
+            if constexpr (INV) return two_pass<A, TS, 9, 8, 8, 16, INV>(j, st);
+            else return two_pass<A, TS, 8, 16, 9, 8, INV>(j, st);
         default: return set_error(MFHE_EUNSUPPORTED, "NTT supports log_n <= 17");
     }
 }
