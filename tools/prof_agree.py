@@ -24,8 +24,10 @@ def main():
     # forward pass kernels: template argument INV (7th) == false
     fwd = [r for r in rows if r["Kernel_Name"].split("<")[1].split(",")[6].strip() == "false"]
     N, L, B = bench["config"]["N"], bench["config"]["limbs"], bench["config"]["batch_per_gpu"]
-    chunk_polys = max(1, (192 << 20) // (L * N * 8))
-    C = -(-B // chunk_polys)
+    # chunks per call as the bench reports them ("mfhe_ntt_fwd call = C chunks x ..."), i.e. from the context's
+    # MFHE_OPT_NTT_CHUNK_BYTES
+    import re
+    C = int(re.search(r"= (\d+) chunks", bench["roofline"]["kernel"]).group(1))
     per = 2 * C
     calls = [fwd[i * per:(i + 1) * per] for i in range(W + S)][W:]
     kern_ms = [sum(int(r["End_Timestamp"]) - int(r["Start_Timestamp"]) for r in c) / 1e6 for c in calls]
