@@ -797,6 +797,13 @@ static int decode_sharded_impl(mfhe_ctx* c, mfhe_ctx* call, mfhe_comm* comm, int
     if (512 % G) return set_error(MFHE_EINVAL, "sharded decode: the communicator size must divide 512 lanes");
     if (call->L != (c->limbs_total ? c->limbs_total : c->L) || call->L != c->L * G)
         return set_error(MFHE_EINVAL, "sharded decode: ctx_all must hold the G * L_shard moduli of the whole set");
+    // the exchange layout puts rank g's limbs at [g L, (g + 1) L) of ctx_all: the shard must be exactly that
+    if (c->limb_base != rank * c->L)
+        return set_error(MFHE_EINVAL, "sharded decode: this rank's shard must start at limb rank * L_shard "
+                                      "(mfhe_ctx_set_limb_shard)");
+    for (int k = 0; k < c->L; ++k)
+        if (call->moduli[(size_t)(rank * c->L + k)] != c->moduli[(size_t)k])
+            return set_error(MFHE_EINVAL, "sharded decode: the shard's moduli differ from ctx_all's limbs rank * L_shard..");
     uint64_t* coeff = pb->get<uint64_t>(g.words);
     double2* ccx = pb->get<double2>(g.cnt);
     double2* ecx = pb->get<double2>(g.cnt);

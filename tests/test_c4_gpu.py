@@ -116,3 +116,20 @@ def test_limb_shard_rejects_bad_ranges(mfhe, full):
         c.set_limb_shard(0, 3)
     c.set_limb_shard(12, 16)
     c.close()
+
+
+def test_sharded_decode_rejects_mismatched_parameter_sets(mfhe, orc, full):
+    """ctx_all must hold this rank's moduli at limbs rank * L_shard..: a different prime set of the same size
+    is an error (not silently wrong messages)."""
+    import torch
+    other = orc.gen_primes(34, 197376, L)                 # 16 different primes
+    assert set(other).isdisjoint(full["moduli"])
+    c_bad = mfhe.Context(other, N_LOG, mfhe.CONV_PHANTOM)
+    comm = mfhe.Comm.from_id(mfhe.Comm.unique_id(), 1, 0)
+    try:
+        out = torch.empty_like(full["mt"])
+        with pytest.raises(mfhe.MfheError):
+            full["ctx"].decrypt_and_decode_sharded(c_bad, comm, "allgather", full["cre"], full["cim"], full["sk"], out)
+    finally:
+        comm.close()
+        c_bad.close()
