@@ -76,7 +76,9 @@ struct mfhe_ctx {
     int ntt_plan = 0;
     int ntt_wg_per_cu = 16;  // NTT pass grid: workgroups per CU (0 = occupancy, 16 = one tile per WG; measured best)
     int ntt_pack = 0;        // MFHE_OPT_NTT_PACK (measured slower, kept opt-in: DESIGN.md §3.1)
-    int ntt_prefetch = 0;    // persistent NTT passes: prefetch the next tile's raw data (MFHE_OPT_NTT_PREFETCH)
+    // MFHE_OPT_NTT_PREFETCH: 1 = persistent passes load the next tile into registers first (slower, r01);
+    // 2 (default) = FP64 forward column pass with the next tile's LDS-DMA in flight (ntt_coldb.hpp, +0.5% C3, r02)
+    int ntt_prefetch = 2;
     int num_cus = 256;
     int ntt_fused = 0;       // N = 2^15..2^17: both passes in one launch (MFHE_OPT_NTT_FUSED)
     int ntt_fused_lag = 2;   // pass-2 lag in polynomials per XCD queue

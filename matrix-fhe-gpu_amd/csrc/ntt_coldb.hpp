@@ -1,0 +1,176 @@
+// ntt_coldb.hpp -- forward column pass of the two-pass NTT (first 8 stages, 16-column tiles, N = 2^15..2^17)
+// with the next tile's LDS-DMA in flight while the current tile's butterflies run.
+//
+// Why: the column pass reads the transform input from HBM and is the slower of the two passes (98 vs 82 us
+// per 240 MiB chunk at C3, profiles/r02_kernel_stats.csv).  In the plain pass a workgroup loads a tile,
+// waits, computes and stores, so only the workgroups that happen to be in their load phase have bytes in
+// flight.  Here every workgroup keeps one 32 KiB tile landing in LDS at all times: two tile buffers,
+// tile t + 1 is DMA'd into one while tile t is transformed in the other.
+//
+// Counted waits.  vmcnt is in order on gfx950, so "tile t has landed" is s_waitcnt vmcnt(n) with n = the
+// vector-memory operations issued after tile t's DMA: the previous tile's 16 stores and the next tile's
+// 8 DMA instructions.  Nothing else in the loop touches vector memory: the twiddles of a limb (15 shared
+// by the workgroup, 15 per thread) are loaded into registers when the limb changes, followed by
+// vmcnt(0).  The DMA is issued by the builtin; the ISA is checked to carry no compiler wait that would
+// cover the prefetch.
+//
+// Same transform, same reduction schedule and same intermediate as NttPass<..., COLS, !INV, OUT_RAW>:
+// the block pass that follows is unchanged, and the output is bit-identical (tests/test_ntt_gpu.py).
+#pragma once
+#include "ntt_kernels.hpp"
+
+namespace mfhe {
+
+struct ColDb {
+    static constexpr int LOG_G = 8, LOG_R = 4, NG = 16;
+    using Gm = Geo<LOG_G, LOG_R>;
+    static constexpr int R = Gm::R, TG = Gm::TG, GS = Gm::GS;
+    static constexpr int NT = NG * TG;                 // 256 threads
+    static constexpr int BUF = NG * GS;                // u64 words per tile buffer (exchange layout, 34,944 B)
+    static constexpr size_t LDS_BYTES = 2 * (size_t)BUF * sizeof(uint64_t);
+    static constexpr int kDmaOps = 32768 / (NT * 16);  // 16-B DMA instructions per thread per tile (8)
+    static_assert(Gm::NR == 2 && TG == 16, "two rounds of four stages");
+};
+
+// tile (row-major [256 rows][16 columns] image, 128 B per row) -> buf by LDS-DMA, 16 B per lane
+__device__ __forceinline__ void coldb_dma(const char* tile, size_t row_bytes, uint64_t* buf, uint32_t w, uint32_t lane) {
+    typedef __attribute__((address_space(3))) void* lds_vp;
+#pragma unroll
+    for (int i = 0; i < ColDb::kDmaOps; ++i) {
+        const uint32_t q = (i * (ColDb::NT / 64) + w) * 64 + lane;   // chunk: row q / 8, part q % 8
+        const char* src = tile + (size_t)(q >> 3) * row_bytes + (q & 7) * 16;
+        __builtin_amdgcn_global_load_lds((const void*)src,
+                                         (lds_vp)((char*)buf + (size_t)(i * (ColDb::NT / 64) + w) * 1024), 16, 0,
+                                         MFHE_NTT_CPOL_IN);
+    }
+}
+
+template <int N>
+__device__ __forceinline__ void vm_wait() {
+    static_assert(N >= 0 && N < 64, "vmcnt immediate");
+    asm volatile("s_waitcnt vmcnt(%0)" ::"n"(N) : "memory");
+}
+
+// LDS-only workgroup barrier: __syncthreads() also carries a workgroup release fence, i.e. a vmcnt(0) that
+// would wait for the prefetch in flight.  Every cross-thread hand-off in this kernel goes through LDS
+// (exchanges) or is ordered by an explicit vm_wait (DMA'd tiles), so lgkmcnt(0) + s_barrier suffices.
+__device__ __forceinline__ void lds_barrier() { asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory"); }
+
+template <class TS>
+__global__ __launch_bounds__(ColDb::NT, 1) void ntt_col_db_kernel(PassArgs<TS> a) {
+    using A = ArithF64;
+    using C = ColDb;
+    using Gm = C::Gm;
+    extern __shared__ __attribute__((aligned(16))) uint64_t lds[];
+    const uint32_t t = threadIdx.x, gl = t % C::NG, tau = t / C::NG, w = t >> 6, lane = t & 63;
+    const uint32_t nb = a.nblocks;
+    uint32_t lt = blockIdx.x;
+    if (lt >= nb) return;
+    const int logS = a.logN - C::LOG_G;
+    const size_t row_bytes = (size_t)8 << logS;
+    auto locate = [&](uint32_t l) {
+        return tile_loc<C::LOG_G, C::NG, true, true>(a.data, a.batch, a.nl, a.start_limb, a.logN, 0, xcd_remap(l, nb), gl);
+    };
+    auto tile_ptr = [&](const TileLoc& L) { return (const char*)(L.base + (L.off0 - gl)); };
+
+    TileLoc L0 = locate(lt);
+    uint64_t* base = L0.base;   // current tile: polynomial base, element offset of its first row, limb
+    uint32_t off0 = L0.off0;
+    int lmod = L0.mod;
+    coldb_dma(tile_ptr(L0), row_bytes, lds, w, lane);
+    int cur = 0, mod = -1;
+    bool first = true;
+    double q = 0.0, qinv = 0.0;
+    double tw0[15], tw1[15];   // round 0: tw[1..15] (shared); round 1: ((16 + tau) << e) + j, e = 3 - bb
+    while (true) {
+        const uint32_t nlt = lt + gridDim.x;
+        const bool more = nlt < nb;   // workgroup-uniform
+        if (lmod != mod) {
+            mod = lmod;
+            const LimbConst lc = a.limbs[mod];
+            q = lc.qf;
+            qinv = lc.qinv;
+            const double* tw = a.tw.p + ((size_t)mod << a.logN);
+#pragma unroll
+            for (int j = 0; j < 15; ++j) tw0[j] = tw[1 + j];
+#pragma unroll
+            for (int e = 0; e < 4; ++e)
+#pragma unroll
+                for (int j = 0; j < (1 << e); ++j) tw1[(1 << e) - 1 + j] = tw[((16 + tau) << e) + j];
+            vm_wait<0>();   // twiddles in registers (also drains tile t's DMA and the previous stores)
+            // re-define the twiddle registers by an (empty) asm after the wait: the compiler's own wait tracking
+            // would otherwise keep these loads pending into the butterflies and put a vmcnt(0) there, which
+            // also waits for the next tile's DMA
+#pragma unroll
+            for (int j = 0; j < 15; ++j) {
+                asm volatile("" : "+v"(tw0[j]));
+                asm volatile("" : "+v"(tw1[j]));
+            }
+        }
+        lds_barrier();   // every thread is done with the other buffer (previous tile's exchange reads)
+        uint64_t* nbase = base;
+        uint32_t noff0 = off0;
+        int nmod = lmod;
+        if (more) {
+            const TileLoc Ln = locate(nlt);
+            nbase = Ln.base;
+            noff0 = Ln.off0;
+            nmod = Ln.mod;
+            coldb_dma(tile_ptr(Ln), row_bytes, lds + (cur ^ 1) * C::BUF, w, lane);
+        }
+        // this thread's part of tile t has landed: newer than its DMA are the previous tile's R stores and the
+        // next tile's DMA instructions
+        if (first) {
+            if (more) vm_wait<C::kDmaOps>();
+            else vm_wait<0>();
+        } else {
+            if (more) vm_wait<C::R + C::kDmaOps>();
+            else vm_wait<C::R>();
+        }
+        lds_barrier();   // ... and every other thread's part
+        first = false;
+
+        uint64_t* buf = lds + (size_t)cur * C::BUF;
+        uint64_t* my = buf + (size_t)gl * C::GS;
+        const A ar(LimbConst{0, q, qinv, 0});
+        double x[C::R];
+#pragma unroll
+        for (int k = 0; k < C::R; ++k) x[k] = A::from_u64(buf[(size_t)Gm::g_of(0, tau, k) * C::NG + gl]);
+        // round 0: stages 0..3 (register bits 3..0), twiddles shared by the workgroup
+        static_for<0, 4>([&](auto bi) {
+            constexpr int bb = 3 - decltype(bi)::value, e = 3 - bb, half = 1 << bb;
+#pragma unroll
+            for (int k = 0; k < C::R; ++k) {
+                if (k & half) continue;
+                ar.ct(x[k], x[k + half], tw0[(1 << e) - 1 + (k >> (bb + 1))]);
+            }
+        });
+        lds_barrier();
+#pragma unroll
+        for (int k = 0; k < C::R; ++k) my[Gm::pad(Gm::g_of(0, tau, k))] = A::to_raw(x[k]);
+        lds_barrier();
+#pragma unroll
+        for (int k = 0; k < C::R; ++k) x[k] = ar.round_reduce(A::from_raw(my[Gm::pad(Gm::g_of(1, tau, k))]));
+        // round 1: stages 4..7, twiddles per thread
+        static_for<0, 4>([&](auto bi) {
+            constexpr int bb = 3 - decltype(bi)::value, e = 3 - bb, half = 1 << bb;
+#pragma unroll
+            for (int k = 0; k < C::R; ++k) {
+                if (k & half) continue;
+                ar.ct(x[k], x[k + half], tw1[(1 << e) - 1 + (k >> (bb + 1))]);
+            }
+        });
+        // intermediate (raw doubles, centred), the same words NttPass<COLS, OUT_RAW> writes
+#pragma unroll
+        for (int k = 0; k < C::R; ++k)
+            base[off0 | ((uint32_t)Gm::g_of(1, tau, k) << logS)] = A::to_raw(ar.reduce(x[k]));
+        if (!more) break;
+        lt = nlt;
+        base = nbase;
+        off0 = noff0;
+        lmod = nmod;
+        cur ^= 1;
+    }
+}
+
+}  // namespace mfhe

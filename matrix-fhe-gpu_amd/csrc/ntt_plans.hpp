@@ -12,6 +12,7 @@
 #include <algorithm>
 
 #include "mfhe_ctx.hpp"
+#include "ntt_coldb.hpp"
 #include "ntt_fused.hpp"
 
 namespace mfhe {
@@ -66,11 +67,11 @@ static int launch_pass(const NttJob<TS>& j, int s0, hipStream_t st) {
     a.nblocks = (uint32_t)nb;
     const bool need_lds = (Gm::NR > 1) || BREV;
     const size_t lds = need_lds ? (size_t)NG * Gm::GS * sizeof(uint64_t) : 0;
-    auto kern = j.prefetch ? ntt_pass_kernel<A, TS, LOG_G, LOG_R, NG, COLS, INV, IN_RAW, OUT_RAW, TWIST, BREV, UNI, true, PACK>
+    auto kern = j.prefetch == 1 ? ntt_pass_kernel<A, TS, LOG_G, LOG_R, NG, COLS, INV, IN_RAW, OUT_RAW, TWIST, BREV, UNI, true, PACK>
                            : ntt_pass_kernel<A, TS, LOG_G, LOG_R, NG, COLS, INV, IN_RAW, OUT_RAW, TWIST, BREV, UNI, false, PACK>;
     // persistent grid: resident workgroups only (occupancy query cached per instantiation), a multiple of 8
     static int occ_cache[2] = {0, 0};
-    int& occ = occ_cache[j.prefetch ? 1 : 0];
+    int& occ = occ_cache[j.prefetch == 1 ? 1 : 0];
     if (occ == 0) {
         int o = 0;
         if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&o, kern, NT, lds) != hipSuccess || o < 1) o = 1;
@@ -82,6 +83,38 @@ static int launch_pass(const NttJob<TS>& j, int s0, hipStream_t st) {
     const uint32_t grid = (uint32_t)std::min<uint64_t>(nb, cap);
     hipLaunchKernelGGL(kern, dim3(grid), dim3(NT), lds, st, a);
     MFHE_CHECK_LAUNCH("ntt_pass_kernel launch");
+    return MFHE_OK;
+}
+
+// forward column pass with the next tile's DMA in flight (ntt_coldb.hpp), MFHE_OPT_NTT_PREFETCH = 2
+static int launch_col_db(const NttJob<TwSrcF>& j, hipStream_t st) {
+    using C = ColDb;
+    const uint64_t npl = j.batch * (uint64_t)j.nl;
+    const uint64_t nb = npl << (j.logN - C::LOG_G - 4);   // 16-column tiles: 2^(logN - 8) / 16 per polynomial
+    if (nb == 0) return MFHE_OK;
+    if (nb > 0xFFFFFFFFull || npl >= 0xFFFFFFFFull)
+        return set_error(MFHE_EINVAL, "NTT batch too large for one launch (batch * nlimbs must be < 2^32)");
+    PassArgs<TwSrcF> a{};
+    a.data = j.data;
+    a.tw = j.tw;
+    a.limbs = j.limbs;
+    a.batch = j.batch;
+    a.nl = j.nl;
+    a.start_limb = j.start_limb;
+    a.logN = j.logN;
+    a.s0 = 0;
+    a.nblocks = (uint32_t)nb;
+    static int occ = 0;
+    if (occ == 0) {
+        int o = 0;
+        if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&o, ntt_col_db_kernel<TwSrcF>, C::NT, C::LDS_BYTES) != hipSuccess || o < 1) o = 1;
+        occ = o;
+    }
+    const int per_cu = j.wg_per_cu > 0 ? std::min(j.wg_per_cu, occ) : occ;
+    const uint64_t cap = std::max<uint64_t>(8, ((uint64_t)per_cu * j.num_cus) & ~7ull);
+    const uint32_t grid = (uint32_t)std::min<uint64_t>(nb, cap);
+    hipLaunchKernelGGL(ntt_col_db_kernel<TwSrcF>, dim3(grid), dim3(C::NT), C::LDS_BYTES, st, a);
+    MFHE_CHECK_LAUNCH("ntt_col_db_kernel launch");
     return MFHE_OK;
 }
 
@@ -134,6 +167,9 @@ static int two_pass_chunk(const NttJob<TS>& c, int pass, hipStream_t st) {
             if (pass == 0) return launch_pass<A, TS, LOG_GA, 4, NGA, true, false, false, true, false, false, true, true>(c, 0, st);
             return launch_pass<A, TS, LOG_GB, 4, NGB, false, false, true, false, false, false, true, true>(c, LOG_GA, st);
         }
+    }
+    if constexpr (!INV && std::is_same<A, ArithF64>::value && LOG_GA == 8 && NGA == 16) {
+        if (pass == 0 && c.prefetch == 2 && c.limbs) return launch_col_db(c, st);
     }
     if (!INV) {
         if (pass == 0) return launch_pass<A, TS, LOG_GA, 4, NGA, true, false, false, true, false, false, true>(c, 0, st);

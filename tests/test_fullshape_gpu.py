@@ -64,7 +64,7 @@ def _check(got, want, what):
                         f"vs {F.top_digest(want)})"
 
 
-def _run_ntt_config(mfhe, orc, dig, name, arith=0, fused=0):
+def _run_ntt_config(mfhe, orc, dig, name, arith=0, fused=0, prefetch=None):
     import torch
     cfg = F.NTT_CONFIGS[name]
     N = 1 << cfg["log_n"]
@@ -75,6 +75,8 @@ def _run_ntt_config(mfhe, orc, dig, name, arith=0, fused=0):
         ctx.set_arith(arith)
     if fused:
         ctx.set_option(OPT_FUSED, 1)
+    if prefetch is not None:   # default: 2 (DMA-prefetch forward column pass); 0 = the plain column pass
+        ctx.set_option(mfhe.OPT_NTT_PREFETCH, prefetch)
     B, nl, st = cfg["batch"], cfg["nl"], cfg["start"]
     per = nl * N
     step = F.CHUNK_POLYS[cfg["log_n"]]
@@ -96,17 +98,19 @@ def test_c2_full_shape(mfhe, orc, dig):
     _run_ntt_config(mfhe, orc, dig, "c2")
 
 
-@pytest.mark.parametrize("arith,fused", [(0, 0), (2, 0), (0, 1)], ids=["f64", "u64", "f64-fused"])
-def test_c3_full_shape(mfhe, orc, dig, arith, fused):
-    _run_ntt_config(mfhe, orc, dig, "c3", arith, fused)
+@pytest.mark.parametrize("arith,fused,prefetch", [(0, 0, None), (2, 0, None), (0, 1, None), (0, 0, 0)],
+                         ids=["f64", "u64", "f64-fused", "f64-plain-colpass"])
+def test_c3_full_shape(mfhe, orc, dig, arith, fused, prefetch):
+    _run_ntt_config(mfhe, orc, dig, "c3", arith, fused, prefetch)
 
 
 def test_c3_60bit_primes_full_shape(mfhe, orc, dig):
     _run_ntt_config(mfhe, orc, dig, "c3u60")
 
 
-def test_c5_shard_full_shape(mfhe, orc, dig):
-    _run_ntt_config(mfhe, orc, dig, "c5shard")
+@pytest.mark.parametrize("prefetch", [None, 0], ids=["default", "plain-colpass"])
+def test_c5_shard_full_shape(mfhe, orc, dig, prefetch):
+    _run_ntt_config(mfhe, orc, dig, "c5shard", prefetch=prefetch)
 
 
 def test_c3_encode_ntt_intt_decode_full_shape(mfhe, orc, dig):

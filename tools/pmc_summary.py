@@ -43,9 +43,12 @@ def main():
     kernels = {}
     tot = {"fwd": [0.0, 0.0], "inv": [0.0, 0.0]}
     for k in fetch:
-        if "ntt_pass_kernel" not in k:
+        if "ntt_col_db_kernel" in k:
+            inv = False                     # the DMA-prefetch column pass is forward only
+        elif "ntt_pass_kernel" in k:
+            inv = k.split("<")[1].split(",")[6].strip() == "true"   # template arg INV
+        else:
             continue
-        inv = k.split("<")[1].split(",")[6].strip() == "true"   # template arg INV
         rb = fetch[k][0] * 2 * 1024          # corrected read bytes, all dispatches
         wb = write[k][0] * 1024
         kernels[k] = {"dispatches": fetch[k][1], "read_bytes_per_dispatch": rb / fetch[k][1],

@@ -19,10 +19,13 @@ from pathlib import Path
 def main():
     d, log, S, W, out = Path(sys.argv[1]), sys.argv[2], int(sys.argv[3]), int(sys.argv[4]), sys.argv[5]
     bench = next(json.loads(l) for l in open(log) if l.startswith("{"))
-    rows = [r for r in csv.DictReader(open(d / "run_kernel_trace.csv")) if "ntt_pass_kernel" in r["Kernel_Name"]]
+    rows = [r for r in csv.DictReader(open(d / "run_kernel_trace.csv"))
+            if "ntt_pass_kernel" in r["Kernel_Name"] or "ntt_col_db_kernel" in r["Kernel_Name"]]
     rows.sort(key=lambda r: int(r["Start_Timestamp"]))
-    # forward pass kernels: template argument INV (7th) == false
-    fwd = [r for r in rows if r["Kernel_Name"].split("<")[1].split(",")[6].strip() == "false"]
+    # forward pass kernels: the DMA-prefetch column pass (forward only), and ntt_pass_kernel with template
+    # argument INV (7th) == false
+    fwd = [r for r in rows if "ntt_col_db_kernel" in r["Kernel_Name"]
+           or r["Kernel_Name"].split("<")[1].split(",")[6].strip() == "false"]
     N, L, B = bench["config"]["N"], bench["config"]["limbs"], bench["config"]["batch_per_gpu"]
     # chunks per call as the bench reports them ("mfhe_ntt_fwd call = C chunks x ..."), i.e. from the context's
     # MFHE_OPT_NTT_CHUNK_BYTES
