@@ -15,6 +15,16 @@
 #include "ntt_coldb.hpp"
 #include "ntt_fused.hpp"
 
+// Groups (contiguous rows) per block-pass workgroup.  N = 2^16: 4 rows (64 threads, 8.7 KiB LDS) rather than 16
+// (256 threads, 34.9 KiB): the block pass gains from residency and 16-row tiles are LDS-bound at 4 per CU;
+// C3 +0.9% forward / +1.4% inverse (profiles/r02_block_ng.txt).
+#ifndef MFHE_NTT_NGB16
+#define MFHE_NTT_NGB16 4
+#endif
+#ifndef MFHE_NTT_NGB17
+#define MFHE_NTT_NGB17 4    // N = 2^17 forward: 512-element rows per block-pass workgroup (8 -> 4: +0.9% C5 shard)
+#endif
+
 namespace mfhe {
 
 enum class Kind { Phantom, GL, Cyclic };
@@ -305,13 +315,16 @@ static int run_phantom(const NttJob<TS>& j, hipStream_t st) {
         case 13: return two_pass<A, TS, 7, 32, 6, 64, INV>(j, st);
         case 14: return two_pass<A, TS, 7, 32, 7, 32, INV>(j, st);
         case 15: return two_pass<A, TS, 8, 16, 7, 32, INV>(j, st);
-        case 16: return two_pass<A, TS, 8, 16, 8, 16, INV>(j, st);
+        case 16:
+            // the packed intermediate's units are laid out for 16-row block tiles
+            if (!INV && j.pack) return two_pass<A, TS, 8, 16, 8, 16, INV>(j, st);
+            return two_pass<A, TS, 8, 16, 8, MFHE_NTT_NGB16, INV>(j, st);
         // N = 2^17: the forward column pass takes 8 stages on 16-column tiles (128-B row segments) and the block
         // pass 9; the inverse keeps 9 column + 8 block stages.  Measured per direction (profiles/r02_n17_split.txt):
         // forward +5%, inverse -2.5% with the other split.
         case 17:
             if constexpr (INV) return two_pass<A, TS, 9, 8, 8, 16, INV>(j, st);
-            else return two_pass<A, TS, 8, 16, 9, 8, INV>(j, st);
+            else return two_pass<A, TS, 8, 16, 9, MFHE_NTT_NGB17, INV>(j, st);
         default: return set_error(MFHE_EUNSUPPORTED, "NTT supports log_n <= 17");
     }
 }
