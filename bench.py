@@ -40,6 +40,7 @@ def parse():
     ap.add_argument("--ntt-chunk", type=int, default=None, help="MFHE_OPT_NTT_CHUNK_BYTES override (tuning)")
     ap.add_argument("--ntt-fused", type=int, default=None, help="MFHE_OPT_NTT_FUSED override (tuning)")
     ap.add_argument("--ntt-pack", type=int, default=None, help="MFHE_OPT_NTT_PACK override (tuning)")
+    ap.add_argument("--ntt-plan", type=int, default=None, help="MFHE_OPT_NTT_PLAN override (tuning)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-pipeline", action="store_true",
                     help="skip the reference-geometry pipeline and other-config NTT lines (N=1 only)")
@@ -460,7 +461,7 @@ def main():
     if args.arith:
         ctx.set_arith(args.arith)
     for opt, val in ((4, args.ntt_wg), (5, args.ntt_prefetch), (mfhe.OPT_NTT_CHUNK_BYTES, args.ntt_chunk),
-                     (6, args.ntt_fused), (mfhe.OPT_NTT_PACK, args.ntt_pack)):
+                     (6, args.ntt_fused), (mfhe.OPT_NTT_PACK, args.ntt_pack), (mfhe.OPT_NTT_PLAN, args.ntt_plan)):
         if val is not None:
             ctx.set_option(opt, val)
     stream = torch.cuda.current_stream()

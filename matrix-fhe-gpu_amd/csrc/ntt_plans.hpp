@@ -21,6 +21,9 @@
 #ifndef MFHE_NTT_NGB16
 #define MFHE_NTT_NGB16 4
 #endif
+#ifndef MFHE_NTT_NGB14
+#define MFHE_NTT_NGB14 32   // N = 2^14 two-pass plan (MFHE_OPT_NTT_PLAN = 2): 128-element rows per block-pass workgroup
+#endif
 #ifndef MFHE_NTT_NGB17
 #define MFHE_NTT_NGB17 4    // N = 2^17 forward: 512-element rows per block-pass workgroup (8 -> 4: +0.9% C5 shard)
 #endif
@@ -313,7 +316,7 @@ static int run_phantom(const NttJob<TS>& j, hipStream_t st) {
     switch (j.logN) {
         case 12: return two_pass<A, TS, 6, 64, 6, 64, INV>(j, st);
         case 13: return two_pass<A, TS, 7, 32, 6, 64, INV>(j, st);
-        case 14: return two_pass<A, TS, 7, 32, 7, 32, INV>(j, st);
+        case 14: return two_pass<A, TS, 7, 32, 7, MFHE_NTT_NGB14, INV>(j, st);
         case 15: return two_pass<A, TS, 8, 16, 7, 32, INV>(j, st);
         case 16:
             // the packed intermediate's units are laid out for 16-row block tiles
