@@ -22,7 +22,7 @@
 #define MFHE_NTT_NGB16 4
 #endif
 #ifndef MFHE_NTT_NGB14
-#define MFHE_NTT_NGB14 32   // N = 2^14 two-pass plan (MFHE_OPT_NTT_PLAN = 2): 128-element rows per block-pass workgroup
+#define MFHE_NTT_NGB14 8    // N = 2^14 two-pass plan: 128-element rows per block-pass workgroup (32 -> 8)
 #endif
 #ifndef MFHE_NTT_NGB17
 #define MFHE_NTT_NGB17 4    // N = 2^17 forward: 512-element rows per block-pass workgroup (8 -> 4: +0.9% C5 shard)
@@ -304,7 +304,10 @@ static int fused(const NttJob<TS>& j, hipStream_t st) {
 
 template <class A, class TS, bool INV>
 static int run_phantom(const NttJob<TS>& j, hipStream_t st) {
-    const bool two = j.logN > 14 || (j.plan == 2 && j.logN >= 12);
+    // auto: N = 2^14 runs two passes (7 + 7, 8-row block tiles): at C2 +1% forward, +7% inverse over the single
+    // pass, which holds one 2^14 polynomial per CU (139 KiB of LDS) and cannot overlap loads with butterflies
+    // (profiles/r02_c2_plans2.txt)
+    const bool two = j.logN > 14 || (j.plan == 2 && j.logN >= 12) || (j.plan == 0 && j.logN == 14);
     if (!two) return run_single<A, TS, INV, false>(j, st);
     if (j.ctx && j.ctx->ntt_fused && j.logN >= 15) {
         switch (j.logN) {
