@@ -21,6 +21,9 @@
 #ifndef MFHE_NTT_NGB16
 #define MFHE_NTT_NGB16 4
 #endif
+#ifndef MFHE_NTT_NGA14
+#define MFHE_NTT_NGA14 16   // N = 2^14 two-pass plan: columns per column-pass workgroup (16: 128-B row segments, +5% C2 fwd over 32)
+#endif
 #ifndef MFHE_NTT_NGB14
 #define MFHE_NTT_NGB14 8    // N = 2^14 two-pass plan: 128-element rows per block-pass workgroup (32 -> 8)
 #endif
@@ -322,7 +325,7 @@ static int run_phantom(const NttJob<TS>& j, hipStream_t st) {
     switch (j.logN) {
         case 12: return two_pass<A, TS, 6, 64, 6, 64, INV>(j, st);
         case 13: return two_pass<A, TS, 7, 32, 6, 64, INV>(j, st);
-        case 14: return two_pass<A, TS, 7, 32, 7, MFHE_NTT_NGB14, INV>(j, st);
+        case 14: return two_pass<A, TS, 7, MFHE_NTT_NGA14, 7, MFHE_NTT_NGB14, INV>(j, st);
         case 15: return two_pass<A, TS, 8, 16, 7, 32, INV>(j, st);
         case 16:
             // the packed intermediate's units are laid out for 16-row block tiles
