@@ -27,6 +27,9 @@
 #ifndef MFHE_NTT_NGB14
 #define MFHE_NTT_NGB14 8    // N = 2^14 two-pass plan: 128-element rows per block-pass workgroup (32 -> 8)
 #endif
+#ifndef MFHE_NTT_NGA17I
+#define MFHE_NTT_NGA17I 8   // N = 2^17 inverse: columns per column-pass workgroup (second pass, 9 stages)
+#endif
 #ifndef MFHE_NTT_NGB17I
 #define MFHE_NTT_NGB17I 4   // N = 2^17 inverse: 256-element rows per block-pass workgroup (first pass, reads the input)
 #endif
@@ -335,7 +338,7 @@ static int run_phantom(const NttJob<TS>& j, hipStream_t st) {
         // pass 9; the inverse keeps 9 column + 8 block stages.  Measured per direction (profiles/r02_n17_split.txt):
         // forward +5%, inverse -2.5% with the other split.
         case 17:
-            if constexpr (INV) return two_pass<A, TS, 9, 8, 8, MFHE_NTT_NGB17I, INV>(j, st);
+            if constexpr (INV) return two_pass<A, TS, 9, MFHE_NTT_NGA17I, 8, MFHE_NTT_NGB17I, INV>(j, st);
             else return two_pass<A, TS, 8, 16, 9, MFHE_NTT_NGB17, INV>(j, st);
         default: return set_error(MFHE_EUNSUPPORTED, "NTT supports log_n <= 17");
     }
