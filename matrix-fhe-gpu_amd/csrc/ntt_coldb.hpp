@@ -21,24 +21,31 @@
 
 namespace mfhe {
 
+#ifndef MFHE_NTT_COLDB_NG
+#define MFHE_NTT_COLDB_NG 16   // columns per tile: 16 (128-B row segments, 2 workgroups/CU) or 32 (256 B, 1/CU)
+#endif
+
 struct ColDb {
-    static constexpr int LOG_G = 8, LOG_R = 4, NG = 16;
+    static constexpr int LOG_G = 8, LOG_R = 4, NG = MFHE_NTT_COLDB_NG;
+    static constexpr int LOG_NG = NG == 32 ? 5 : 4;
+    static constexpr int CPR = NG / 2;                 // 16-B chunks per tile row
     using Gm = Geo<LOG_G, LOG_R>;
     static constexpr int R = Gm::R, TG = Gm::TG, GS = Gm::GS;
     static constexpr int NT = NG * TG;                 // 256 threads
     static constexpr int BUF = NG * GS;                // u64 words per tile buffer (exchange layout, 34,944 B)
     static constexpr size_t LDS_BYTES = 2 * (size_t)BUF * sizeof(uint64_t);
-    static constexpr int kDmaOps = 32768 / (NT * 16);  // 16-B DMA instructions per thread per tile (8)
+    static constexpr int kDmaOps = 256 * NG * 8 / (NT * 16);  // 16-B DMA instructions per thread per tile (8)
     static_assert(Gm::NR == 2 && TG == 16, "two rounds of four stages");
+    static_assert(NG == 16 || NG == 32, "16 or 32 columns per tile");
 };
 
-// tile (row-major [256 rows][16 columns] image, 128 B per row) -> buf by LDS-DMA, 16 B per lane
+// tile (row-major [256 rows][NG columns] image, 8 NG bytes per row) -> buf by LDS-DMA, 16 B per lane
 __device__ __forceinline__ void coldb_dma(const char* tile, size_t row_bytes, uint64_t* buf, uint32_t w, uint32_t lane) {
     typedef __attribute__((address_space(3))) void* lds_vp;
 #pragma unroll
     for (int i = 0; i < ColDb::kDmaOps; ++i) {
-        const uint32_t q = (i * (ColDb::NT / 64) + w) * 64 + lane;   // chunk: row q / 8, part q % 8
-        const char* src = tile + (size_t)(q >> 3) * row_bytes + (q & 7) * 16;
+        const uint32_t q = (i * (ColDb::NT / 64) + w) * 64 + lane;   // chunk: row q / CPR, part q % CPR
+        const char* src = tile + (size_t)(q / ColDb::CPR) * row_bytes + (q % ColDb::CPR) * 16;
         __builtin_amdgcn_global_load_lds((const void*)src,
                                          (lds_vp)((char*)buf + (size_t)(i * (ColDb::NT / 64) + w) * 1024), 16, 0,
                                          MFHE_NTT_CPOL_IN);

@@ -112,7 +112,7 @@ static int launch_pass(const NttJob<TS>& j, int s0, hipStream_t st) {
 static int launch_col_db(const NttJob<TwSrcF>& j, hipStream_t st) {
     using C = ColDb;
     const uint64_t npl = j.batch * (uint64_t)j.nl;
-    const uint64_t nb = npl << (j.logN - C::LOG_G - 4);   // 16-column tiles: 2^(logN - 8) / 16 per polynomial
+    const uint64_t nb = npl << (j.logN - C::LOG_G - C::LOG_NG);   // NG-column tiles: 2^(logN - 8) / NG per polynomial
     if (nb == 0) return MFHE_OK;
     if (nb > 0xFFFFFFFFull || npl >= 0xFFFFFFFFull)
         return set_error(MFHE_EINVAL, "NTT batch too large for one launch (batch * nlimbs must be < 2^32)");
