@@ -601,9 +601,10 @@ def main():
             alg_bytes = 16.0 * N * batch * L       # 8N read + 8N write per NTT
             ach = alg_bytes / (res["fwd_ev_ms"] * 1e-3) / 1e9
             chunk_polys = max(1, ctx.get_option(mfhe.OPT_NTT_CHUNK_BYTES) // (L * N * 8))
-            nchunks = -(-batch // chunk_polys) if log_n > 14 else 1
-            kname = (f"mfhe_ntt_fwd call = {nchunks} chunks x (column pass + block pass) ntt_pass_kernel launches"
-                     if log_n > 14 else "mfhe_ntt_fwd call = 1 single-pass ntt_pass_kernel launch")
+            nchunks = -(-batch // chunk_polys) if log_n >= 14 else 1
+            kname = (f"mfhe_ntt_fwd call = {nchunks} chunks x (column pass ntt_col_db_kernel + block pass "
+                     f"ntt_pass_kernel) launches" if log_n >= 14 else
+                     "mfhe_ntt_fwd call = 1 single-pass ntt_pass_kernel launch")
             out["roofline"] = {"bound": "hbm", "kernel": kname,
                                "achieved": round(ach, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                                "frac": round(ach / HBM_PEAK_GBS, 4), "traffic": None,

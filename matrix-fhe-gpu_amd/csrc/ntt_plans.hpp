@@ -213,6 +213,7 @@ static int two_pass(const NttJob<TS>& j, hipStream_t st) {
     uint64_t cb = j.batch;
     if (j.chunk_bytes > 0) cb = std::max<uint64_t>(1, (uint64_t)j.chunk_bytes / poly_bytes);
     const uint64_t nch = (j.batch + cb - 1) / cb;
+    cb = (j.batch + nch - 1) / nch;   // equal chunks (no small tail chunk paying two launches for little work)
     auto chunk = [&](uint64_t k) {
         NttJob<TS> c = j;
         const uint64_t b0 = k * cb;
