@@ -45,7 +45,8 @@ def parse():
     ap.add_argument("--no-pipeline", action="store_true",
                     help="skip the reference-geometry pipeline and other-config NTT lines (N=1 only)")
     ap.add_argument("--cpu-seconds", type=float, default=10.0)
-    ap.add_argument("--only", default="all", help="all | ntt | crt | recombine | c4 (profiling)")
+    ap.add_argument("--no-c5", action="store_true", help="skip the BASELINE C5 residue-shard line")
+    ap.add_argument("--only", default="all", help="all | ntt | crt | recombine | c4 | c5 (profiling)")
     ap.add_argument("--recombine-batch", type=int, default=256,
                     help="polys per step for the residue-shard INTT + CRT recombine line (0 = skip)")
     return ap.parse_args()
@@ -102,40 +103,75 @@ def pmc_traffic(N, L, batch):
     return best
 
 
+def prof_trace(N, L, batch):
+    """The committed rocprofv3 kernel trace of the bench command (tools/prof_agree.py ->
+    profiles/*ntt_rocprof_vs_event*.json) for this shape: the latest round's file wins."""
+    import glob
+    best = None
+    for f in sorted(glob.glob(str(ROOT / "profiles" / "*ntt_rocprof_vs_event*.json"))):
+        try:
+            d = json.load(open(f))
+        except (OSError, ValueError):
+            continue
+        sh = d.get("shape", {})
+        if (sh.get("N"), sh.get("limbs"), sh.get("batch")) == (N, L, batch) and "rocprof_kernel_ms_per_transform" in d:
+            best = dict(d, file=Path(f).name)
+    return best
+
+
 def other_configs_line(reps=10):
     """The other BASELINE.json NTT shapes on this one GPU (parity cases, not the headline): C2 whole, and the
-    per-GPU residue shard of C4 (4 GPUs) and C5 (8 GPUs).  Forward and inverse NTT/s, HIP events."""
+    per-GPU residue shard of C4 (4 GPUs) and C5 (8 GPUs).  Forward and inverse NTT/s, HIP events.
+
+    C2's 128 MiB batch fits the 256 MiB Infinity Cache, so re-transforming one buffer measures the cache, not
+    HBM: C2 is timed both ways -- one resident buffer ("cache_resident") and 8 rotating
+    buffers of 128 MiB (1 GiB, each evicted before its next use: the HBM figure, which is the one `frac_fwd`
+    is quoted on)."""
     import torch
     import mfhe
     res = {}
-    for name, log_n, L, lg, batch in (("C2: N=2^14 L=4 batch 256", 14, 4, 4, 256),
-                                     ("C4 shard: N=2^16 L=16 (4 of 16 limbs) batch 1024", 16, 16, 4, 1024),
-                                     ("C5 shard: N=2^17 L=32 (4 of 32 limbs) batch 4096", 17, 32, 4, 4096)):
+    for name, log_n, L, lg, batch, nbuf in (("C2: N=2^14 L=4 batch 256", 14, 4, 4, 256, 8),
+                                           ("C4 shard: N=2^16 L=16 (4 of 16 limbs) batch 1024", 16, 16, 4, 1024, 1),
+                                           ("C5 shard: N=2^17 L=32 (4 of 32 limbs) batch 4096", 17, 32, 4, 4096, 1)):
         N = 1 << log_n
         moduli = gen_moduli(50, 1 << (log_n + 2), L)
         ctx = mfhe.Context(moduli, log_n, mfhe.CONV_PHANTOM)
-        d = torch.empty(batch * lg * N, dtype=torch.int64, device="cuda")
         qt = torch.tensor(moduli[:lg], dtype=torch.int64, device="cuda").repeat_interleave(N).repeat(batch)
-        d.random_(0, 2 ** 62).remainder_(qt)
+        bufs = []
+        for _ in range(nbuf):
+            d = torch.empty(batch * lg * N, dtype=torch.int64, device="cuda")
+            d.random_(0, 2 ** 62).remainder_(qt)
+            bufs.append(d)
         del qt
-        out = {}
-        for kind, fn in (("fwd", ctx.ntt_fwd), ("inv", ctx.ntt_inv)):
-            fn(d, batch=batch, start_limb=0, nlimbs=lg)
+
+        def rate(fn, nb):
+            for k in range(nb):
+                fn(bufs[k], batch=batch, start_limb=0, nlimbs=lg)
             torch.cuda.synchronize()
             e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
             e0.record()
-            for _ in range(reps):
-                fn(d, batch=batch, start_limb=0, nlimbs=lg)
+            n = reps * nb
+            for k in range(n):
+                fn(bufs[k % nb], batch=batch, start_limb=0, nlimbs=lg)
             e1.record()
             torch.cuda.synchronize()
-            ms = e0.elapsed_time(e1) / reps
-            rate = batch * lg / (ms * 1e-3)
-            out[f"{kind}_NTT_per_s"] = round(rate)
-            out[f"{kind}_alg_GBps"] = round(16.0 * N * rate / 1e9, 1)
+            return batch * lg / (e0.elapsed_time(e1) / n * 1e-3)
+
+        out = {}
+        for kind, fn in (("fwd", ctx.ntt_fwd), ("inv", ctx.ntt_inv)):
+            r = rate(fn, nbuf)
+            out[f"{kind}_NTT_per_s"] = round(r)
+            out[f"{kind}_alg_GBps"] = round(16.0 * N * r / 1e9, 1)
+            if nbuf > 1:
+                rc = rate(fn, 1)
+                out[f"cache_resident_{kind}_NTT_per_s"] = round(rc)
+                out[f"cache_resident_{kind}_alg_GBps"] = round(16.0 * N * rc / 1e9, 1)
         out["frac_fwd"] = round(out["fwd_alg_GBps"] / HBM_PEAK_GBS, 4)
         out["working_set_GiB"] = round(batch * lg * N * 8 / 2 ** 30, 3)
+        if nbuf > 1:
+            out["rotating_buffers"] = f"{nbuf} x {out['working_set_GiB']} GiB (HBM figure; cache_resident_*: one buffer)"
         res[name] = out
-        del d
+        del bufs
         ctx.close()
     return res
 
@@ -307,6 +343,110 @@ def c4_line(world, rank, comm, barrier, reps=5):
             "scaling": "strong (one batch for all ranks)", **out}
 
 
+def c5_line(world, rank, barrier, timed, backend, reps=2, recv_gib=2.0):
+    """BASELINE C5: N = 2^17, L = 32 x 50-bit primes (bootstrapping depth), batch 4096, residues sharded over
+    the G ranks: rank g owns limbs [g*32/G, (g+1)*32/G) of every polynomial (16 GiB per GPU at G = 8, the
+    whole 128 GiB at G = 1).  Strong scaling: the problem is fixed, G divides it.  One step =
+      * forward + inverse NTT of the shard (no communication);
+      * the CRT recombine of the whole batch: RCCL exchange + sharded wide-CRT compose -> f64/delta of this
+        rank's polys, chunked over polys so the receive buffer stays <= recv_gib (mfhe.dist.chunk_plan).
+    The shard holds the residues of real messages (|z| < 1, delta = 2^35), as a decode does.
+    Curves: NTT alone, NTT + recombine by all-to-all (each rank receives only its polys' missing limbs,
+    (G-1)/G^2 of the set), NTT + recombine by all-gather (every rank receives (G-1)/G of the set, 112 GiB at
+    G = 8: run chunk by chunk, never as one buffer).  G = 1: the compose is local (no exchange)."""
+    import torch
+    import mfhe
+    from mfhe import dist as mdist
+    log_n, L, batch = 17, 32, 4096
+    N = 1 << log_n
+    if L % world or batch % world:
+        return {"skipped": f"world {world} does not divide 32 limbs / 4096 polys"}
+    moduli = gen_moduli(50, 1 << (log_n + 2), L)
+    s0, lg = mdist.limb_range(L, world, rank)
+    ctx = mfhe.Context(moduli[s0:s0 + lg], log_n, mfhe.CONV_PHANTOM)   # this rank's limbs: NTT tables
+    ctx_all = mfhe.Context(moduli, log_n, mfhe.CONV_PHANTOM)           # all 32: the CRT tables
+    dev = torch.device("cuda", torch.cuda.current_device())
+    stream = torch.cuda.current_stream()
+    shard = torch.empty(batch * lg * N, dtype=torch.int64, device=dev)
+    g = torch.Generator(device=dev).manual_seed(0x4D46484500000005)
+    cpg = 256                                    # decompose in 256-poly pieces (same messages on every rank)
+    z = torch.empty(cpg * N, dtype=torch.float64, device=dev)
+    for p0 in range(0, batch, cpg):
+        z.uniform_(-1.0, 1.0, generator=g)
+        ctx.rns_decompose(z, shard[p0 * lg * N:(p0 + cpg) * lg * N], cpg, N, stream=stream)
+    del z
+    out = torch.empty(batch // world * N, dtype=torch.float64, device=dev)
+    comm = mfhe.Comm.create() if world > 1 and backend == "nccl" else None
+    modes = ("alltoall", "allgather") if world > 1 else ("local",)
+    # chunk so one exchange receives <= recv_gib: all-to-all receives cp/G polys x 32 limbs, all-gather cp x 32
+    per_poly = L * N * 8
+    chunks = {"alltoall": int(recv_gib * 2 ** 30 // per_poly) * world, "allgather": int(recv_gib * 2 ** 30 // per_poly),
+              "local": batch}
+    if comm is not None:
+        for m in modes:
+            ctx_all.crt_recombine_reserve(comm, m, max(world, chunks[m] // world * world), N)
+
+    def ntt():
+        ctx.ntt_fwd(shard, batch=batch, stream=stream)
+        ctx.ntt_inv(shard, batch=batch, stream=stream)
+
+    res = {}
+    w, _ = timed(ntt, reps, 1)
+    t_ntt = w / reps
+    res["ntt_fwd_inv_ms"] = round(t_ntt * 1e3, 3)
+    res["ntt_NTT_per_s"] = round(2 * batch * L / t_ntt)     # both directions, all ranks
+    for m in modes:
+        def step(m=m):
+            ntt()
+            if m == "local":
+                ctx_all.crt_compose_f64(shard, out, batch, N, stream=stream)
+            else:
+                mdist.crt_recombine_chunked(ctx_all, shard, batch, N, m, chunks[m], out, stream=stream, comm=comm)
+        if comm is None and m != "local":
+            return {"skipped": f"the C5 recombine needs the RCCL communicator (backend {backend})"}
+        w, _ = timed(step, reps, 1)
+        t = w / reps
+        recv = (world - 1) / world * batch * per_poly / (world if m == "alltoall" else 1)
+        res[m] = {"ms": round(t * 1e3, 3), "recombine_ms": round((t - t_ntt) * 1e3, 3),
+                  "polys_per_s": round(batch / t), "chunk_polys": min(batch, chunks[m]),
+                  "recv_GiB_per_gpu": round(recv / 2 ** 30, 2),
+                  "recv_GBps_per_gpu": round(recv / max(t - t_ntt, 1e-9) / 1e9, 1)}
+    # spot check of the last mode run: the first output row of every rank is poly rank * (chunk / G) (poly 0
+    # on rank 0), whose message is regenerated here: |err| <= 2^-36 (llround to delta = 2^35, exact CRT)
+    own0 = mdist.owned_polys(batch, world, rank, chunks[modes[-1]])[0]
+    g.manual_seed(0x4D46484500000005)
+    z = torch.empty(cpg * N, dtype=torch.float64, device=dev).uniform_(-1.0, 1.0, generator=g)
+    torch.cuda.synchronize()
+    res["max_err_first_row"] = float((out[:N] - z[own0 * N:(own0 + 1) * N]).abs().max())
+    res["check_2^-36"] = res["max_err_first_row"] <= 2.0 ** -36
+    if comm is not None:
+        comm.close()
+    ctx.close()
+    ctx_all.close()
+    return {"workload": f"C5: N=2^17, L=32 x 50-bit primes, batch 4096, limbs sharded over {world} GPU(s) "
+                        f"({lg} per GPU): fwd+inv NTT of the shard, then chunked RCCL recombine + wide-CRT "
+                        f"compose -> f64 of this rank's 4096/{world} polys",
+            "scaling": "strong (one problem for all ranks)", **res}
+
+
+def cpu_quota():
+    """CPUs this process may use per the cgroup CPU quota (cpu.max / cfs_quota_us), or None if unlimited."""
+    try:
+        q, p = open("/sys/fs/cgroup/cpu.max").read().split()[:2]
+        if q != "max":
+            return max(1, int(q) // int(p))
+    except (OSError, ValueError):
+        pass
+    try:
+        q = int(open("/sys/fs/cgroup/cpu/cpu.cfs_quota_us").read())
+        p = int(open("/sys/fs/cgroup/cpu/cpu.cfs_period_us").read())
+        if q > 0:
+            return max(1, q // p)
+    except (OSError, ValueError):
+        pass
+    return None
+
+
 def cpu_baseline(log_n, moduli, seconds):
     """The reference's CPU path restated (oracle/, test infrastructure; the reference itself has no runnable
     CPU path), timed on this box's host cores on bounded samples of each workload:
@@ -315,13 +455,22 @@ def cpu_baseline(log_n, moduli, seconds):
         big -> f64 HE.cu:1007-1027) on the same shape, all cores and 1 core;
       * the reference's own GL NTT (ntt_core.cu:462-481) at its geometry (n = 64, L = 11, 512 x 64 polys);
       * the C1 (N = 2^12, L = 1, single poly) and C2 (N = 2^14, L = 4, batch 256) forward NTT.
-    `cores` = OpenMP threads used for the all-core figures; nproc and the affinity mask are printed too (on
-    the GPU box nproc counts the whole machine, the process may be confined to fewer)."""
+
+    Cores.  `cores` = the OpenMP threads of the all-core figures, set explicitly: the CPUs this process may
+    use, i.e. min(affinity mask, cgroup quota, the harness's per-GPU CPU share).  On the GPU box nproc and the
+    affinity mask count the whole host (256) while one GPU's job is given a 16-CPU share (OMP_NUM_THREADS=16
+    there, and its worker-pool rule): 256 threads on 16 CPUs would time the scheduler, not the oracle.  All
+    three numbers are printed with the reason."""
     import numpy as np
     sys.path.insert(0, str(ROOT / "tests"))
     import oracle
     aff = len(os.sched_getaffinity(0))
-    threads = int(os.environ.get("OMP_NUM_THREADS", aff))
+    quota = cpu_quota()
+    share = int(os.environ.get("OMP_NUM_THREADS", "0") or 0) or None
+    threads = min(x for x in (aff, quota, share) if x)
+    reason = ("affinity mask" if threads == aff else "cgroup CPU quota" if threads == quota
+              else "per-GPU CPU share (OMP_NUM_THREADS set by the harness; affinity counts the whole host)")
+    oracle.L.orc_set_threads(threads)
     N, L = 1 << log_n, len(moduli)
     per = max(0.5, seconds / 8)          # seconds per measured figure
     rng = np.random.default_rng(0)
@@ -341,7 +490,7 @@ def cpu_baseline(log_n, moduli, seconds):
         return (rng.integers(0, 2 ** 63, (b, L_, n), dtype=np.uint64) % q).ravel()
 
     m64 = np.array(moduli, np.uint64)
-    b = 16
+    b = 64
     x = residues(b, L, N, moduli)
     ntt_all = rate(lambda: oracle.L.orc_phantom_fwd(oracle.P(x), b, L, log_n, oracle.P(m64)), b * L)
     x1 = x[: 2 * L * N].copy()
@@ -365,7 +514,7 @@ def cpu_baseline(log_n, moduli, seconds):
             com(oracle.P(r), npoly, L, N, oracle.P(m64), W, oracle.P(mag), oracle.P(neg))
             oracle.L.orc_big_to_f64(oracle.P(mag), oracle.P(neg), npoly * N, W, delta, oracle.P(out), 1)
         return rate(f, npoly)
-    crt_all, crt_1 = enc_crt(32, False), enc_crt(2, True)
+    crt_all, crt_1 = enc_crt(64, False), enc_crt(2, True)
 
     # reference GL NTT at the reference geometry: n = 64, the 11 reference moduli, 512 x 64 polys
     import mfhe
@@ -380,10 +529,11 @@ def cpu_baseline(log_n, moduli, seconds):
     c2 = residues(256, 4, 1 << 14, m14)
     c2r = rate(lambda: oracle.phantom_fwd(c2, 4, 14, m14), 256 * 4)
     return {"value": ntt_all, "unit": "NTT/s", "cores": threads, "kind": "port",
-            "nproc": os.cpu_count(), "affinity_cores": aff,
+            "nproc": os.cpu_count(), "affinity_cores": aff, "cgroup_quota_cores": quota,
+            "omp_num_threads_env": share, "cores_reason": reason,
             "sample": f"forward NTT N=2^{log_n} x L={L} (oracle phantom Harvey NTT, OpenMP {threads} threads), "
                       f"~{per:.1f} s per figure; the headline workload is 1024 polys x {L} limbs, sampled at "
-                      f"{b} polys per call",
+                      f"{b} polys ({b * L} NTTs) per call",
             "one_core_NTT_per_s": ntt_1,
             "encode_crt_ops_per_s": {"all_cores": crt_all, "one_core": crt_1,
                                      "op": f"decompose + wide CRT compose + f64 of one N=2^{log_n} poly, L={L}, W={W}"},
@@ -501,8 +651,10 @@ def main():
     if args.only in ("all", "ntt"):
         wall, ev_ms = timed(lambda: ctx.ntt_fwd(data, batch=batch, stream=stream), args.steps, args.warmup)
         res["fwd_wall"], res["fwd_ev_ms"] = wall, ev_ms
-        wall_i, ev_i = timed(lambda: ctx.ntt_inv(data, batch=batch, stream=stream), max(1, args.steps // 2), 1)
-        res["inv_ev_ms"] = ev_i
+        # the inverse with exactly the forward's steps and warm-up (the first ~30 ms of calls run in the clock
+        # ramp, profiles/r02_bench_steps.txt, so fewer steps would understate it)
+        wall_i, ev_i = timed(lambda: ctx.ntt_inv(data, batch=batch, stream=stream), args.steps, args.warmup)
+        res["inv_ev_ms"], res["inv_wall"] = ev_i, wall_i
     if args.only in ("all", "crt"):
         # encode+CRT op = one real poly of N coefficients: decompose (f64 -> L residues) + compose (-> f64/delta)
         cb = max(1, batch // 4)
@@ -575,6 +727,11 @@ def main():
             c4 = c4_line(world, rank, c4comm, barrier)
             c4comm.close()
 
+    c5 = None
+    if args.only in ("all", "c5") and not args.no_c5:
+        c5 = c5_line(world, rank, barrier, timed, backend)
+        torch.cuda.empty_cache()
+
     if rank == 0:
         ntts = batch * L * world
         out = {
@@ -617,7 +774,19 @@ def main():
                 out["roofline"]["traffic"] = tr[0]
                 out["roofline"]["traffic_source"] = f"profiles/{tr[1]}"
                 out["roofline"]["traffic_over_algorithmic"] = round(tr[0] / alg_bytes, 3)
-            out["inverse_NTT_per_s"] = batch * L / (res["inv_ev_ms"] * 1e-3) * world
+            out["inverse_NTT_per_s"] = ntts / (res["inv_wall"] / args.steps)
+            out["inverse_over_forward"] = round(out["inverse_NTT_per_s"] / out["value"], 4)
+            tr = prof_trace(N, L, batch)
+            if tr:
+                # per-kernel averages of a committed rocprofv3 --kernel-trace run of this same command
+                # (tools/prof_agree.py): the roofline recomputed from the trace alone
+                out["roofline"]["kernel_ms_per_transform"] = round(tr["rocprof_kernel_ms_per_transform"], 4)
+                out["roofline"]["kernel_trace_frac"] = round(
+                    alg_bytes / (tr["rocprof_kernel_ms_per_transform"] * 1e-3) / 1e9 / HBM_PEAK_GBS, 4)
+                out["roofline"]["kernel_trace_source"] = f"profiles/{tr['file']}"
+                out["roofline"]["kernel_trace_per_kernel_avg_us"] = {
+                    k.split("(")[0].split("<")[0].replace("void mfhe::", ""): round(v["avg_us"], 2)
+                    for k, v in tr["per_kernel"].items()}
         if "crt_ev_ms" in res:
             cb = res["crt_batch"]
             out["encode_crt_ops_per_s"] = cb / (res["crt_ev_ms"] * 1e-3) * world
@@ -626,6 +795,8 @@ def main():
             out["residue_shard_ntt_roundtrip_crt_recombine"] = res["recombine"]
         if c4 is not None:
             out["c4_sharded_pipeline"] = c4
+        if c5 is not None:
+            out["c5_residue_shard"] = c5
         if world == 1 and not args.no_pipeline and args.only == "all":
             out["reference_geometry_pipeline"] = pipeline_line()
             out["other_ntt_configs"] = other_configs_line()

@@ -11,8 +11,9 @@
 //   * table setup is per (n, limbs) context, built once; no static first-caller keying;
 //   * batched single launches replace per-poly / per-lane launch loops;
 //   * the GPU kernels declared as __global__ in encoder.cuh (dequantize_exact_kernel,
-//     crt_compose_centerlift_kernel, mat_mul_kernel_complex) are replaced by the host entry points
-//     below (and mfhe_crt_compose_f64 / mfhe_xy_dft); kernel symbols are not part of this surface.
+//     crt_compose_centerlift_kernel, mat_mul_kernel_complex) are replaced by host entry points
+//     (crt_compose_centerlift below, mfhe_crt_compose_f64, mfhe_xy_dft); kernel symbols are not part of
+//     this surface.
 #pragma once
 #include <hip/hip_complex.h>
 #include <hip/hip_runtime.h>
@@ -119,6 +120,10 @@ void multiply_ciphertexts_raw(const RLWECiphertext& ct1, const RLWECiphertext& c
 // ---- encoders (reference encoder.cuh, batched_encoder.cuh) ----
 void crt_compose_centerlift_big(const uint64_t* d_in_rns, uint64_t* d_out_mag, uint8_t* d_out_neg, int n2, int limbs,
                                 hipStream_t stream = 0);
+// host entry for the __global__ crt_compose_centerlift_kernel (encoder.cu:152-189): the centred value truncated to
+// int64 (low magnitude word, sign applied with wrap), <<<ceil(n2/256), 256>>> over one lane's [limbs][n2]
+void crt_compose_centerlift(const uint64_t* d_in_rns, int64_t* d_out_centered, int n2, int limbs,
+                            hipStream_t stream = 0);
 
 class Encoder {
    public:

@@ -376,6 +376,21 @@ __global__ __launch_bounds__(256) void crt_compose_kernel(CrtArgs a, uint64_t* _
     out_neg[i] = neg ? 1 : 0;
 }
 
+// crt_compose_centerlift_kernel (encoder.cu:152-189): the centred value truncated to its low word,
+// v = (int64)mag[0], out = neg ? -v : v (wrapping, as the reference's int64 negation does on the GPU)
+template <int W>
+__global__ __launch_bounds__(256) void crt_compose_i64_kernel(CrtArgs a, int64_t* __restrict__ out) {
+    const uint64_t i = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x;
+    if (i >= a.total) return;
+    uint64_t p, c;
+    split_index(i, a.ncoeff, a.lg_nc, p, c);
+    uint64_t mag[W];
+    bool neg;
+    compose_one<W>(a.in + p * (uint64_t)a.Lg * a.ncoeff + c, a.ncoeff, a.L, a.Lg, a.shard_stride, a.qmu, a.inv,
+                   a.qinv, a.M, a.Q, a.Qh, mag, neg, a.lf, a.qbig);
+    out[i] = (int64_t)(neg ? (uint64_t)0 - mag[0] : mag[0]);
+}
+
 template <int W>
 __global__ __launch_bounds__(256) void crt_compose_f64_kernel(CrtArgs a, double delta, double* __restrict__ out,
                                                               uint64_t out_stride) {
@@ -465,6 +480,24 @@ extern "C" int mfhe_crt_compose(mfhe_ctx* c, const uint64_t* in, size_t npoly, s
         default: return set_error(MFHE_EUNSUPPORTED, "crt words > 32");
     }
     MFHE_CHECK_LAUNCH("crt_compose_kernel");
+    return MFHE_OK;
+}
+
+extern "C" int mfhe_crt_compose_i64(mfhe_ctx* c, const uint64_t* in, size_t npoly, size_t ncoeff, int64_t* out,
+                                    mfhe_stream_t s) {
+    if (!c) return set_error(MFHE_EINVAL, "null ctx");
+    const uint64_t total = (uint64_t)npoly * ncoeff;
+    if (total == 0) return MFHE_OK;
+    if (!in || !out) return set_error(MFHE_EINVAL, "mfhe_crt_compose_i64: null pointer");
+    const CrtArgs a = crt_args(c, in, npoly, ncoeff);
+    switch (c->W) {
+#define X(w) \
+    case w: hipLaunchKernelGGL(crt_compose_i64_kernel<w>, grid1d(total, 256), dim3(256), 0, (hipStream_t)s, a, out); break;
+        MFHE_W_CASES(X)
+#undef X
+        default: return set_error(MFHE_EUNSUPPORTED, "crt words > 32");
+    }
+    MFHE_CHECK_LAUNCH("crt_compose_i64_kernel");
     return MFHE_OK;
 }
 

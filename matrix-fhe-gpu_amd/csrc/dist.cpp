@@ -19,6 +19,8 @@
 
 #include <cstring>
 #include <mutex>
+#include <string>
+#include <vector>
 #include <type_traits>
 #include <rccl/rccl.h>
 
@@ -75,6 +77,7 @@ struct mfhe_comm {
     int nranks = 1, rank = 0, device = 0;
     void* recv = nullptr;   // receive buffer of the recombine exchange
     size_t recv_bytes = 0;
+    int32_t* flags = nullptr;   // comm_agree: [nranks] gathered verdicts + [1] this rank's
 };
 
 using mfhe::set_error;
@@ -137,6 +140,10 @@ extern "C" int mfhe_comm_destroy(mfhe_comm* c) {
         hipError_t he = hipFree(c->recv);
         if (he != hipSuccess) rc = mfhe::hip_error(he, "hipFree");
     }
+    if (c->flags) {
+        hipError_t he = hipFree(c->flags);
+        if (he != hipSuccess && !rc) rc = mfhe::hip_error(he, "hipFree");
+    }
     if (c->owned && c->comm) {
         ncclResult_t e = rccl().CommDestroy(c->comm);
         if (e != ncclSuccess && !rc) rc = nccl_error(e, "ncclCommDestroy");
@@ -168,6 +175,31 @@ int comm_allgather_bytes(mfhe_comm* c, const void* send, void* recv, size_t byte
     if (int rc = need_rccl()) return rc;
     ncclResult_t e = rccl().AllGather(send, recv, bytes, ncclUint8, c->comm, s);
     return e == ncclSuccess ? MFHE_OK : nccl_error(e, "ncclAllGather");
+}
+int comm_agree(mfhe_comm* c, int local_rc, hipStream_t s) {
+    if (!c) return local_rc ? local_rc : set_error(MFHE_EINVAL, "null comm");
+    if (c->nranks == 1) return local_rc;
+    if (int rc = need_rccl()) return local_rc ? local_rc : rc;
+    const std::string mine = local_rc ? mfhe_last_error() : "";
+    if (!c->flags && hipMalloc(&c->flags, (size_t)(c->nranks + 1) * sizeof(int32_t)) != hipSuccess) {
+        c->flags = nullptr;
+        return local_rc ? local_rc : set_error(MFHE_ENOMEM, "comm_agree: hipMalloc failed");
+    }
+    std::vector<int32_t> all((size_t)c->nranks, 0);
+    const int32_t v = local_rc;
+    hipError_t he = hipMemcpyAsync(c->flags + c->nranks, &v, sizeof v, hipMemcpyHostToDevice, s);
+    if (he != hipSuccess) return mfhe::hip_error(he, "comm_agree");
+    ncclResult_t e = rccl().AllGather(c->flags + c->nranks, c->flags, 1, ncclInt32, c->comm, s);
+    if (e != ncclSuccess) return nccl_error(e, "comm_agree: ncclAllGather");
+    he = hipMemcpyAsync(all.data(), c->flags, all.size() * sizeof(int32_t), hipMemcpyDeviceToHost, s);
+    if (he == hipSuccess) he = hipStreamSynchronize(s);
+    if (he != hipSuccess) return mfhe::hip_error(he, "comm_agree");
+    if (local_rc) return set_error(local_rc, mine);
+    for (int r = 0; r < c->nranks; ++r)
+        if (all[(size_t)r])
+            return set_error(MFHE_EINVAL, "rank " + std::to_string(r) + " rejected the sharded call (code " +
+                                              std::to_string(all[(size_t)r]) + "); see that rank's error");
+    return MFHE_OK;
 }
 int comm_size_rank(const mfhe_comm* c, int* size, int* rank) {
     if (!c) return set_error(MFHE_EINVAL, "null comm");

@@ -794,16 +794,6 @@ static int decode_sharded_impl(mfhe_ctx* c, mfhe_ctx* call, mfhe_comm* comm, int
     const Geo2 g = geo(c);
     int G = 1, rank = 0;
     RC(comm_size_rank(comm, &G, &rank));
-    if (512 % G) return set_error(MFHE_EINVAL, "sharded decode: the communicator size must divide 512 lanes");
-    if (call->L != (c->limbs_total ? c->limbs_total : c->L) || call->L != c->L * G)
-        return set_error(MFHE_EINVAL, "sharded decode: ctx_all must hold the G * L_shard moduli of the whole set");
-    // the exchange layout puts rank g's limbs at [g L, (g + 1) L) of ctx_all: the shard must be exactly that
-    if (c->limb_base != rank * c->L)
-        return set_error(MFHE_EINVAL, "sharded decode: this rank's shard must start at limb rank * L_shard "
-                                      "(mfhe_ctx_set_limb_shard)");
-    for (int k = 0; k < c->L; ++k)
-        if (call->moduli[(size_t)(rank * c->L + k)] != c->moduli[(size_t)k])
-            return set_error(MFHE_EINVAL, "sharded decode: the shard's moduli differ from ctx_all's limbs rank * L_shard..");
     uint64_t* coeff = pb->get<uint64_t>(g.words);
     double2* ccx = pb->get<double2>(g.cnt);
     double2* ecx = pb->get<double2>(g.cnt);
@@ -971,28 +961,45 @@ extern "C" int mfhe_decrypt_and_decode(mfhe_ctx* c, const uint64_t* cre, const u
     return decode_impl(c, er, ei, msg, (hipStream_t)s, &inner);
 }
 
+// Every argument check of a sharded decode, run by each rank on its own arguments.
 static int sharded_args(mfhe_ctx* c, mfhe_ctx* call, mfhe_comm* comm, const void* a, const void* b, const void* m) {
     RC(need_wcrt(c));
-    if (!call || !comm || !a || !b || !m) return set_error(MFHE_EINVAL, "sharded decode: null pointer");
+    if (!call || !a || !b || !m) return set_error(MFHE_EINVAL, "sharded decode: null pointer");
     if (call->N != c->N) return set_error(MFHE_EINVAL, "sharded decode: ctx_all has another ring degree");
-    return MFHE_OK;
+    // the compose divides by ctx_all's delta: another scale would give silently wrong messages
+    if (call->delta != c->delta) return set_error(MFHE_EINVAL, "sharded decode: ctx_all has another scale (delta)");
+    int G = 1, rank = 0;
+    RC(comm_size_rank(comm, &G, &rank));
+    if (512 % G) return set_error(MFHE_EINVAL, "sharded decode: the communicator size must divide 512 lanes");
+    if (call->L != (c->limbs_total ? c->limbs_total : c->L) || call->L != c->L * G)
+        return set_error(MFHE_EINVAL, "sharded decode: ctx_all must hold the G * L_shard moduli of the whole set");
+    // the exchange layout puts rank g's limbs at [g L, (g + 1) L) of ctx_all: the shard must be exactly that
+    if (c->limb_base != rank * c->L)
+        return set_error(MFHE_EINVAL, "sharded decode: this rank's shard must start at limb rank * L_shard "
+                                      "(mfhe_ctx_set_limb_shard)");
+    for (int k = 0; k < c->L; ++k)
+        if (call->moduli[(size_t)(rank * c->L + k)] != c->moduli[(size_t)k])
+            return set_error(MFHE_EINVAL, "sharded decode: the shard's moduli differ from ctx_all's limbs rank * L_shard..");
+    RC(ensure_xy(c));
+    return ensure_ws(c);
 }
 extern "C" int mfhe_decode_sharded(mfhe_ctx* c, mfhe_ctx* call, mfhe_comm* comm, int mode, const uint64_t* re,
                                    const uint64_t* im, double* msg, mfhe_stream_t s) {
-    RC(sharded_args(c, call, comm, re, im, msg));
-    RC(ensure_xy(c));
-    RC(ensure_ws(c));
+    if (!comm) return set_error(MFHE_EINVAL, "sharded decode: null communicator");
+    // the ranks agree on the verdict before any collective: one rank's bad arguments fail every rank instead of
+    // leaving the others blocked in the exchange
+    RC(comm_agree(comm, sharded_args(c, call, comm, re, im, msg), (hipStream_t)s));
     Bump b{(char*)c->ws};
     return decode_sharded_impl(c, call, comm, mode, re, im, msg, (hipStream_t)s, &b);
 }
 extern "C" int mfhe_decrypt_and_decode_sharded(mfhe_ctx* c, mfhe_ctx* call, mfhe_comm* comm, int mode,
                                                const uint64_t* cre, const uint64_t* cim, const uint64_t* sk, double* msg,
                                                mfhe_stream_t s) {
-    RC(sharded_args(c, call, comm, cre, cim, msg));
-    if (!(c->conv & MFHE_CONV_PHANTOM)) return set_error(MFHE_ENOTREADY, "decrypt needs MFHE_CONV_PHANTOM (X-NTT)");
-    if (!sk) return set_error(MFHE_EINVAL, "sharded decrypt: null key");
-    RC(ensure_xy(c));
-    RC(ensure_ws(c));
+    if (!comm) return set_error(MFHE_EINVAL, "sharded decode: null communicator");
+    int rc = sharded_args(c, call, comm, cre, cim, msg);
+    if (!rc && !(c->conv & MFHE_CONV_PHANTOM)) rc = set_error(MFHE_ENOTREADY, "decrypt needs MFHE_CONV_PHANTOM (X-NTT)");
+    if (!rc && !sk) rc = set_error(MFHE_EINVAL, "sharded decrypt: null key");
+    RC(comm_agree(comm, rc, (hipStream_t)s));
     const Geo2 g = geo(c);
     Bump b{(char*)c->ws};
     uint64_t* er = b.get<uint64_t>(g.words);

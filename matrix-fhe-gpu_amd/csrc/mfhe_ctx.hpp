@@ -21,6 +21,10 @@ int set_error(int code, const std::string& msg);
 // dist.cpp: in-place-capable all-gather of `bytes` per rank over a libmfhe communicator (RCCL)
 int comm_allgather_bytes(mfhe_comm* comm, const void* send, void* recv, size_t bytes, hipStream_t s);
 int comm_size_rank(const mfhe_comm* comm, int* size, int* rank);
+// dist.cpp: every rank's local verdict (0 or an MFHE_* code) exchanged over the communicator (one tiny
+// all-gather + a host sync; nothing for 1 rank).  Returns local_rc if this rank failed, an MFHE_EINVAL naming
+// the failing rank if another did, else MFHE_OK -- so every rank reaches the same decision.
+int comm_agree(mfhe_comm* comm, int local_rc, hipStream_t s);
 int hip_error(hipError_t e, const char* what);
 int ensure_xy(mfhe_ctx* c);   // XY encoder matrices, built on first use (ctx.cpp)
 

@@ -108,6 +108,20 @@ static int launch_pass(const NttJob<TS>& j, int s0, hipStream_t st) {
     return MFHE_OK;
 }
 
+// The column pass's counted vmcnt waits assume its loop issues exactly R stores + kDmaOps DMAs per tile: a build
+// whose kernel spills (scratch loads/stores are vector-memory ops too) would make them too loose.  Checked once
+// per process from the code object's metadata; such a build runs the plain column pass instead
+// (tests/test_isa.py checks the instruction counts of the shipped library).
+static bool col_db_usable() {
+    static int ok = -1;
+    if (ok < 0) {
+        hipFuncAttributes fa{};
+        ok = hipFuncGetAttributes(&fa, reinterpret_cast<const void*>(ntt_col_db_kernel<TwSrcF>)) == hipSuccess &&
+             fa.localSizeBytes == 0;
+    }
+    return ok == 1;
+}
+
 // forward column pass with the next tile's DMA in flight (ntt_coldb.hpp), MFHE_OPT_NTT_PREFETCH = 2
 static int launch_col_db(const NttJob<TwSrcF>& j, hipStream_t st) {
     using C = ColDb;
@@ -191,7 +205,7 @@ static int two_pass_chunk(const NttJob<TS>& c, int pass, hipStream_t st) {
         }
     }
     if constexpr (!INV && std::is_same<A, ArithF64>::value && LOG_GA == 8 && NGA == 16) {
-        if (pass == 0 && c.prefetch == 2 && c.limbs) return launch_col_db(c, st);
+        if (pass == 0 && c.prefetch == 2 && c.limbs && col_db_usable()) return launch_col_db(c, st);
     }
     if (!INV) {
         if (pass == 0) return launch_pass<A, TS, LOG_GA, 4, NGA, true, false, false, true, false, false, true>(c, 0, st);

@@ -94,6 +94,7 @@ _sig("mfhe_inwt_1d", [_vp, _vp, _vp, _vp, _vp, _vp, _sz, _sz, _sz, _sz, _vp])
 _sig("mfhe_rns_decompose", [_vp, _vp, _sz, _sz, _sz, _vp, _vp])
 _sig("mfhe_crt_compose", [_vp, _vp, _sz, _sz, _vp, _vp, _vp])
 _sig("mfhe_crt_to_f64", [_vp, _vp, _vp, _sz, _vp, _sz, _vp])
+_sig("mfhe_crt_compose_i64", [_vp, _vp, _sz, _sz, _vp, _vp])
 _sig("mfhe_crt_compose_f64", [_vp, _vp, _sz, _sz, _vp, _sz, _vp])
 _sig("mfhe_crt_compose_f64_sharded", [_vp, _vp, ctypes.c_int, _sz, _sz, _sz, _vp, _sz, _vp])
 for _n in ("mfhe_wcrt_fwd", "mfhe_wcrt_inv", "mfhe_wcrt_fwd_vector", "mfhe_wcrt_fwd_centered",
@@ -155,6 +156,13 @@ def _need(t, words, what):
     an out-of-bounds device access)."""
     if t.numel() * t.element_size() < 8 * words:
         raise ValueError(f"{what}: {t.numel()} elements of {t.element_size()} B < {words} words needed")
+
+
+def _need_strided(t, count, stride, what):
+    """An output written at t[i * stride], i < count: (count - 1) * stride + 1 words."""
+    if stride < 1:
+        raise ValueError(f"{what}: stride must be >= 1")
+    _need(t, (count - 1) * stride + 1 if count else 0, what)
 
 
 class _stdout_to_stderr:
@@ -343,12 +351,24 @@ class Context:
         check(lib.mfhe_crt_compose(self._h, _ptr(src), npoly, ncoeff, _ptr(mag), _ptr(neg), _stream_ptr(stream)),
               "crt_compose")
 
+    def crt_compose_i64(self, src, out, npoly, ncoeff, stream=None):
+        """Centred CRT value truncated to int64 (crt_compose_centerlift_kernel, encoder.cu:152-189)."""
+        _need(src, npoly * self.L * ncoeff, "crt_compose_i64 src")
+        _need(out, npoly * ncoeff, "crt_compose_i64 out")
+        check(lib.mfhe_crt_compose_i64(self._h, _ptr(src), npoly, ncoeff, _ptr(out), _stream_ptr(stream)),
+              "crt_compose_i64")
+        return out
+
     def crt_to_f64(self, mag, neg, out, count, out_stride=1, stream=None):
+        _need(mag, count * self.info().crt_words, "crt_to_f64 mag")
+        _need_strided(out, count, out_stride, "crt_to_f64 out")
         check(lib.mfhe_crt_to_f64(self._h, _ptr(mag), _ptr(neg), count, _ptr(out), out_stride, _stream_ptr(stream)),
               "crt_to_f64")
         return out
 
     def crt_compose_f64(self, src, out, npoly, ncoeff, out_stride=1, stream=None):
+        _need(src, npoly * self.L * ncoeff, "crt_compose_f64 src")
+        _need_strided(out, npoly * ncoeff, out_stride, "crt_compose_f64 out")
         check(lib.mfhe_crt_compose_f64(self._h, _ptr(src), npoly, ncoeff, _ptr(out), out_stride, _stream_ptr(stream)),
               "crt_compose_f64")
         return out
@@ -357,6 +377,9 @@ class Context:
     def crt_compose_f64_sharded(self, src, out, nshards, shard_stride, npoly, ncoeff, out_stride=1, stream=None,
                                 src_offset=0):
         """Compose residue shards gathered from `nshards` GPUs in place (see include/mfhe.h)."""
+        _need(src, src_offset + (nshards - 1) * shard_stride + npoly * (self.L // max(nshards, 1)) * ncoeff,
+              "crt_compose_f64_sharded src")
+        _need_strided(out, npoly * ncoeff, out_stride, "crt_compose_f64_sharded out")
         check(lib.mfhe_crt_compose_f64_sharded(self._h, _ptr(src) + 8 * src_offset, nshards, shard_stride, npoly,
                                                ncoeff, _ptr(out), out_stride, _stream_ptr(stream)),
               "crt_compose_f64_sharded")
@@ -369,7 +392,8 @@ class Context:
         g = comm.size
         lg = self.info().num_limbs // g if g else 0
         _need(shard, npoly * lg * ncoeff, "shard")
-        _need(out, (npoly // g) * ncoeff if g else 0, "out")
+        # the kernel writes out[i * out_stride] for i < npoly / G * ncoeff
+        _need_strided(out, (npoly // g) * ncoeff if g else 0, out_stride, "out")
         check(lib.mfhe_crt_recombine_sharded(self._h, comm._h, m, _ptr(shard), npoly, ncoeff, _ptr(out), out_stride,
                                              _stream_ptr(stream)), "crt_recombine_sharded")
         return out

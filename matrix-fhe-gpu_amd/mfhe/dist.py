@@ -56,6 +56,43 @@ def exchange_residues(shard: torch.Tensor, batch: int, lg: int, ncoeff: int, mod
     raise ValueError(f"unknown exchange mode {mode!r}")
 
 
+def chunk_plan(batch: int, world: int, chunk_polys: int) -> list[tuple[int, int, int]]:
+    """Recombine in poly chunks to bound the receive buffer (BASELINE C5: the whole all-gather would be
+    112 GiB per GPU).  Returns [(p0, cp, row0)]: polys [p0, p0 + cp) are exchanged together (cp a multiple of
+    `world`) and this rank's cp / world composed polys land at output rows [row0, row0 + cp / world)."""
+    if batch % world:
+        raise ValueError(f"batch={batch} must be a multiple of world={world}")
+    cp = max(world, chunk_polys // world * world)
+    plan, p0 = [], 0
+    while p0 < batch:
+        c = min(cp, batch - p0)
+        plan.append((p0, c, p0 // world))
+        p0 += c
+    return plan
+
+
+def owned_polys(batch: int, world: int, rank: int, chunk_polys: int) -> list[int]:
+    """Global poly index of each output row of `rank` under chunk_plan (row order)."""
+    out = []
+    for p0, cp, _ in chunk_plan(batch, world, chunk_polys):
+        bs = cp // world
+        out += list(range(p0 + rank * bs, p0 + (rank + 1) * bs))
+    return out
+
+
+def crt_recombine_chunked(ctx, shard: torch.Tensor, batch: int, ncoeff: int, mode: str, chunk_polys: int,
+                          out: torch.Tensor, group=None, stream=None, comm=None) -> torch.Tensor:
+    """crt_recombine over chunk_plan's poly chunks: shard [batch][Lg][ncoeff] -> out [batch/world][ncoeff] f64,
+    rows in owned_polys order.  Each chunk is one exchange + in-place sharded compose."""
+    world = comm.size if comm is not None else dist.get_world_size(group)
+    lg = ctx.info().num_limbs // world
+    for p0, cp, row0 in chunk_plan(batch, world, chunk_polys):
+        sh = shard[p0 * lg * ncoeff:(p0 + cp) * lg * ncoeff]
+        o = out[row0 * ncoeff:(row0 + cp // world) * ncoeff]
+        crt_recombine(ctx, sh, cp, ncoeff, mode, group, out=o, stream=stream, comm=comm)
+    return out
+
+
 def crt_recombine(ctx, shard: torch.Tensor, batch: int, ncoeff: int, mode: str = "allgather", group=None,
                   out: torch.Tensor | None = None, stream=None, comm=None) -> torch.Tensor:
     """Exchange residue shards and compose this rank's batch slice to f64 (centred value / delta).

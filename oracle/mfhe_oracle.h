@@ -100,6 +100,12 @@ void orc_crt_compose(const uint64_t* in, size_t npoly, int L, size_t N, const ui
                      int W, uint64_t* mag, uint8_t* neg);
 void orc_crt_compose_1t(const uint64_t* in, size_t npoly, int L, size_t N, const uint64_t* moduli,
                         int W, uint64_t* mag, uint8_t* neg);
+/* crt_compose_centerlift_kernel (encoder.cu:152-189): centred value truncated to int64 */
+void orc_crt_compose_i64(const uint64_t* in, size_t npoly, int L, size_t N, const uint64_t* moduli, int W,
+                         int64_t* out);
+/* OpenMP threads of the parallel entry points (bench cpu_baseline) */
+void orc_set_threads(int n);
+int orc_max_threads(void);
 /* compose_big_pair_to_complex_by_delta (HE.cu:1007-1027), per value: out[i] = +-big/delta. */
 void orc_big_to_f64(const uint64_t* mag, const uint8_t* neg, size_t count, int W, double delta,
                     double* out, size_t out_stride);

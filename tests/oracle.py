@@ -62,6 +62,9 @@ _s("orc_crt_min_words", [vp, ci], ci)
 _s("orc_crt_tables", [vp, ci, ci, vp, vp, vp, vp], ci)
 for n in ("orc_crt_compose", "orc_crt_compose_1t"):
     _s(n, [vp, sz, ci, sz, vp, ci, vp, vp])
+_s("orc_crt_compose_i64", [vp, sz, ci, sz, vp, ci, vp])
+_s("orc_set_threads", [ci])
+_s("orc_max_threads", [], ci)
 _s("orc_big_to_f64", [vp, vp, sz, ci, ctypes.c_double, vp, sz])
 for n in ("orc_rns_decompose", "orc_rns_decompose_1t"):
     _s(n, [vp, sz, sz, sz, ci, vp, ctypes.c_double, vp])
@@ -178,6 +181,16 @@ def crt_compose(data, npoly, L_, N, moduli, W=None):
     neg = np.zeros(npoly * N, np.uint8)
     L.orc_crt_compose(P(d), npoly, L_, N, P(m), W, P(mag), P(neg))
     return mag.reshape(npoly * N, W), neg
+
+
+def crt_compose_i64(data, npoly, L_, N, moduli, W=None):
+    """encoder.cu:152-189: centred CRT value truncated to int64 (low magnitude word, sign with wrap)."""
+    d = U64(data)
+    m = U64(moduli)
+    W = W or crt_words(moduli)
+    out = np.zeros(npoly * N, np.int64)
+    L.orc_crt_compose_i64(P(d), npoly, L_, N, P(m), W, P(out))
+    return out
 
 
 def big_to_f64(mag, neg, W, delta):

@@ -125,11 +125,16 @@ def test_sharded_decode_rejects_mismatched_parameter_sets(mfhe, orc, full):
     other = orc.gen_primes(34, 197376, L)                 # 16 different primes
     assert set(other).isdisjoint(full["moduli"])
     c_bad = mfhe.Context(other, N_LOG, mfhe.CONV_PHANTOM)
+    # the right primes at another scale: the compose would divide by the wrong delta
+    c_delta = mfhe.Context(full["moduli"], N_LOG, mfhe.CONV_PHANTOM, delta=2.0 ** 30)
     comm = mfhe.Comm.from_id(mfhe.Comm.unique_id(), 1, 0)
     try:
         out = torch.empty_like(full["mt"])
-        with pytest.raises(mfhe.MfheError):
-            full["ctx"].decrypt_and_decode_sharded(c_bad, comm, "allgather", full["cre"], full["cim"], full["sk"], out)
+        for bad in (c_bad, c_delta):
+            with pytest.raises(mfhe.MfheError):
+                full["ctx"].decrypt_and_decode_sharded(bad, comm, "allgather", full["cre"], full["cim"], full["sk"],
+                                                       out)
     finally:
         comm.close()
         c_bad.close()
+        c_delta.close()

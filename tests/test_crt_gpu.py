@@ -83,6 +83,14 @@ def test_crt_compose_and_f64_match_oracle(mfhe, orc):
         ctx.crt_compose_f64(d, f2, npoly, nc, out_stride=2)
         torch.cuda.synchronize()
         np.testing.assert_array_equal(f2.cpu().numpy()[::2], ref, err_msg=name)
+        # truncating int64 centre lift (crt_compose_centerlift_kernel, encoder.cu:152-189): random residues
+        # (wide values, truncated to the low word) and the small-value decode regime
+        i64 = torch.zeros(npoly * nc, dtype=torch.int64, device="cuda")
+        ctx.crt_compose_i64(d, i64, npoly, nc)
+        torch.cuda.synchronize()
+        np.testing.assert_array_equal(i64.cpu().numpy(), orc.crt_compose_i64(data, npoly, len(moduli), nc, moduli, W),
+                                      err_msg=name)
+        np.testing.assert_array_equal(i64.cpu().numpy()[nc + 3:], small[3:], err_msg=name)
 
 
 @pytest.mark.parametrize("nc", [4096, 3001])

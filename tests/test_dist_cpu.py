@@ -135,3 +135,100 @@ def test_c4_decode_exchange(mode, world):
     for p in procs:
         p.join(timeout=60)
     assert res == {r: True for r in range(world)}
+
+
+class _OracleShardCtx:
+    """Stands in for an mfhe.Context in crt_recombine's torch.distributed path on CPU: info().num_limbs and
+    crt_compose_f64_sharded, the latter restated with the oracle over the sharded layout exactly as
+    crt_compose_f64_kernel addresses it (limb k = s * Lg + j at src_offset + s * shard_stride + (p * Lg + j) * n)."""
+
+    class _Info:
+        def __init__(self, L):
+            self.num_limbs = L
+
+    def __init__(self, moduli, delta):
+        self.moduli, self.delta = moduli, delta
+
+    def info(self):
+        return self._Info(len(self.moduli))
+
+    def crt_compose_f64_sharded(self, src, out, nshards, shard_stride, npoly, ncoeff, out_stride=1, stream=None,
+                                src_offset=0):
+        import oracle as O
+        L = len(self.moduli)
+        lg = L // nshards
+        b = src.numpy().view(np.uint64)
+        res = np.empty((npoly, L, ncoeff), np.uint64)
+        for k in range(L):
+            s, j = divmod(k, lg)
+            for p in range(npoly):
+                base = src_offset + s * shard_stride + (p * lg + j) * ncoeff
+                res[p, k] = b[base:base + ncoeff]
+        W = O.crt_words(self.moduli)
+        mag, neg = O.crt_compose(res.ravel(), npoly, L, ncoeff, self.moduli, W)
+        out.view(-1)[::out_stride][:npoly * ncoeff] = torch.from_numpy(O.big_to_f64(mag, neg, W, self.delta))
+        return out
+
+
+def _c5_rank(rank, world, port, mode, chunk, q):
+    """BASELINE C5's exchange at small N: L = 32 limbs sharded over `world` ranks, the recombine chunked over
+    polys (mfhe.dist.crt_recombine_chunked, the bench's c5 line), every rank's output rows = the composed
+    values of the polys owned_polys says it owns."""
+    import sys
+    from pathlib import Path
+    root = Path(__file__).resolve().parent.parent
+    sys.path[:0] = [str(root / "matrix-fhe-gpu_amd"), str(root / "tests")]
+    import torch.distributed as dist
+    from mfhe import dist as mdist
+    import oracle as O
+
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        L, batch, n, delta = 32, 16, 8, 2.0 ** 35
+        moduli = O.gen_primes(50, 1 << 10, L)
+        rng = np.random.default_rng(7)
+        v = rng.integers(-(1 << 52), 1 << 52, (batch, n))
+        full = np.stack([(v.astype(object) % m).astype(np.uint64) for m in moduli], axis=1)   # [batch][L][n]
+        s0, lg = mdist.limb_range(L, world, rank)
+        shard = torch.from_numpy(full[:, s0:s0 + lg, :].astype(np.int64).copy()).view(-1)
+        out = torch.full((batch // world * n,), np.nan, dtype=torch.float64)
+        mdist.crt_recombine_chunked(_OracleShardCtx(moduli, delta), shard, batch, n, mode, chunk, out)
+        own = mdist.owned_polys(batch, world, rank, chunk)
+        want = v[own].ravel().astype(np.float64) / delta
+        ok = len(own) == batch // world and np.array_equal(out.numpy(), want)
+        # every poly is owned by exactly one rank
+        allown = [None] * world
+        dist.all_gather_object(allown, own)
+        ok = ok and sorted(sum(allown, [])) == list(range(batch))
+        q.put((rank, bool(ok)))
+    finally:
+        dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("mode", ["allgather", "alltoall"])
+@pytest.mark.parametrize("world,chunk", [(8, 8), (8, 16), (4, 12), (2, 4)])
+def test_c5_chunked_recombine_layout(mode, world, chunk):
+    """C5 is 8 GPUs: world 8 (one chunk and two chunks of polys), plus 4 and 2 ranks with ragged chunking."""
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_c5_rank, args=(r, world, port, mode, chunk, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    res = dict(q.get(timeout=180) for _ in procs)
+    for p in procs:
+        p.join(timeout=60)
+    assert res == {r: True for r in range(world)}
+
+
+def test_chunk_plan_bounds():
+    import sys
+    from pathlib import Path
+    sys.path.insert(0, str(Path(__file__).resolve().parent.parent / "matrix-fhe-gpu_amd"))
+    from mfhe import dist as mdist
+    assert mdist.chunk_plan(4096, 8, 512) == [(p, 512, p // 8) for p in range(0, 4096, 512)]
+    assert mdist.chunk_plan(20, 4, 6) == [(0, 4, 0), (4, 4, 1), (8, 4, 2), (12, 4, 3), (16, 4, 4)]
+    assert mdist.chunk_plan(12, 2, 8) == [(0, 8, 0), (8, 4, 4)]
+    with pytest.raises(ValueError):
+        mdist.chunk_plan(10, 4, 8)

@@ -1,0 +1,64 @@
+"""CPU check of the shipped code object: the forward column pass's counted waits (csrc/ntt_coldb.hpp).
+
+ntt_col_db_kernel keeps the next tile's LDS-DMA in flight and waits for the current tile with
+`s_waitcnt vmcnt(N)`, N = the vector-memory operations issued after that tile's DMA (16 stores + 8 DMAs).
+That is only right while the compiled kernel issues exactly those: a spill (scratch_* ops), a split store or
+an extra load in the loop would make the waits too loose and the butterflies would read LDS before the DMA
+lands.  This test disassembles the gfx950 code object inside libmfhe.so and pins the kernel's vector-memory
+instruction mix and wait immediates; the library also refuses the kernel at run time if it has scratch
+(ntt_plans.hpp col_db_usable).  Needs only the built library and ROCm's llvm tools (no GPU).
+"""
+import collections
+import re
+import subprocess
+import tempfile
+from pathlib import Path
+
+import pytest
+
+ROOT = Path(__file__).resolve().parent.parent
+LIB = ROOT / "matrix-fhe-gpu_amd" / "libmfhe.so"
+LLVM = Path("/opt/rocm/lib/llvm/bin")
+MAGIC = b"__CLANG_OFFLOAD_BUNDLE__"
+
+
+def _kernel_asm(symbol_re: str) -> str:
+    if not LIB.exists() or not (LLVM / "llvm-objdump").exists():
+        pytest.skip("libmfhe.so or ROCm llvm tools missing")
+    with tempfile.TemporaryDirectory() as td:
+        td = Path(td)
+        fb = td / "fb.bin"
+        subprocess.run([str(LLVM / "llvm-objcopy"), f"--dump-section=.hip_fatbin={fb}", str(LIB)], check=True,
+                       capture_output=True)
+        data = fb.read_bytes()
+        starts = [m.start() for m in re.finditer(re.escape(MAGIC), data)] + [len(data)]
+        for k in range(len(starts) - 1):   # one offload bundle per translation unit, concatenated
+            part, co = td / f"b{k}.bin", td / f"b{k}.co"
+            part.write_bytes(data[starts[k]:starts[k + 1]])
+            r = subprocess.run([str(LLVM / "clang-offload-bundler"), "--unbundle", "--type=o", f"--input={part}",
+                                "--targets=hipv4-amdgcn-amd-amdhsa--gfx950", f"--output={co}"], capture_output=True)
+            if r.returncode or not co.exists() or co.stat().st_size == 0:
+                continue
+            dis = subprocess.run([str(LLVM / "llvm-objdump"), "-d", str(co)], capture_output=True, text=True).stdout
+            m = re.search(r"^[0-9a-f]+ <(" + symbol_re + r")>:\n(.*?)(?:\n\n|\Z)", dis, re.S | re.M)
+            if m:
+                return m.group(2)
+    pytest.fail(f"kernel {symbol_re} not found in {LIB}")
+
+
+def test_column_pass_dma_waits_match_the_instruction_mix():
+    asm = _kernel_asm(r"_ZN4mfhe17ntt_col_db_kernel[^>]*")
+    ops = collections.Counter(re.findall(r"^\s+((?:global|buffer|flat|scratch)_[a-z0-9_]+)", asm, re.M))
+    waits = sorted({int(v) for v in re.findall(r"s_waitcnt[^\n]*vmcnt\((\d+)\)", asm)})
+    # ColDb: kDmaOps = 8 DMA instructions per tile (prologue + loop body), R = 16 stores of the intermediate
+    assert ops["global_load_lds_dwordx4"] == 16, ops
+    assert ops["global_store_dwordx2"] == 16, ops
+    assert not any(k.startswith("scratch_") for k in ops), ops            # no spills
+    assert not any("store" in k for k in ops if k != "global_store_dwordx2"), ops
+    # everything else is the once-per-limb twiddle / constant fetch, followed by vmcnt(0)
+    other = {k: v for k, v in ops.items() if k not in ("global_load_lds_dwordx4", "global_store_dwordx2")}
+    assert set(other) <= {"global_load_dwordx4", "global_load_dwordx2", "global_load_dword"}, ops
+    assert sum(other.values()) <= 24, ops
+    # the counted waits: 8 (first tile behind the next DMA), 16 (last tile behind the stores), 24 (both)
+    assert set(waits) <= {0, 8, 16, 24}, waits
+    assert {8, 16, 24} <= set(waits), waits
