@@ -30,7 +30,8 @@ timeout -k 10 300 rocprofv3 --kernel-trace --stats -d "$OUT/prof" -o run --outpu
     > "$OUT/prof.log" 2>&1 || { echo "rocprof failed rc=$?"; tail -20 "$OUT/prof.log"; exit 4; }
 P=$(find "$OUT/prof" -name "run_kernel_trace.csv" | head -1)
 python3 "$ROOT/tools/prof_agree.py" "$(dirname "$P")" "$OUT/prof.log" $STEPS $WARM "$OUT/ntt_rocprof_vs_event.json" \
-    | head -12 || exit 5
+    > "$OUT/prof_agree.out" 2>&1 || { echo "prof_agree failed"; tail -5 "$OUT/prof_agree.out"; exit 5; }
+grep -E "ms_per_transform|kernel_over_event" "$OUT/prof_agree.out" || true
 
 for C in FETCH_SIZE WRITE_SIZE; do
   if [ -x "$ROOT/tools/microbench/pmc_calib" ]; then
