@@ -7,7 +7,7 @@ counters are in KiB; FETCH_SIZE reports exactly half of the bytes read by coales
 Infinity-Cache hits, so "traffic" is L2<->fabric bytes (HBM + MALL).
 
 usage: tools/pmc_summary.py <pmc dir> <fwd transforms> <inv transforms> <algorithmic bytes/transform> <out.json>
-       [N L batch]   (the shape bench.py measured; bench.py only uses a file whose config matches its run)
+       [N L batch [command]]   (the shape bench.py measured; bench.py only uses a file whose config matches its run)
 """
 import collections
 import csv
@@ -59,7 +59,8 @@ def main():
     out = {}
     if len(sys.argv) > 8:
         out["config"] = {"N": int(sys.argv[6]), "limbs": int(sys.argv[7]), "batch": int(sys.argv[8]),
-                         "command": "tools/pmc_run.sh (bench.py --only ntt --steps 2 --warmup 1)"}
+                         "command": sys.argv[9] if len(sys.argv) > 9 else
+                         "tools/pmc_run.sh (bench.py --only ntt --steps 2 --warmup 1)"}
     out.update({"calibration": calib, "kernels": kernels, "algorithmic_bytes_per_transform": alg})
     for key, n in (("fwd", nf), ("inv", ni)):
         r, w = tot[key][0] / n, tot[key][1] / n
