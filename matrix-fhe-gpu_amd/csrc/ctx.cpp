@@ -568,7 +568,13 @@ extern "C" int mfhe_ctx_set_option(mfhe_ctx* c, int opt, int64_t v) {
             c->ntt_pack = (int)v;
             return MFHE_OK;
         case MFHE_OPT_NTT_FUSED:
-            if (v < 0 || v > 1) return set_error(MFHE_EINVAL, "fused must be 0 or 1");
+            if (v < 0 || v > 2) return set_error(MFHE_EINVAL, "fused must be 0, 1 or 2");
+            if (v) {
+                int dev = 0;
+                if (hipGetDevice(&dev) == hipSuccess && dev != c->device)
+                    return set_error(MFHE_EINVAL, "fused: set the option on the context's device");
+                if (int rc = xcc_census(c)) return rc;
+            }
             c->ntt_fused = (int)v;
             return MFHE_OK;
         case MFHE_OPT_NTT_FUSED_LAG:

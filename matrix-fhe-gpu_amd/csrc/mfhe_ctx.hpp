@@ -27,6 +27,7 @@ int comm_size_rank(const mfhe_comm* comm, int* size, int* rank);
 int comm_agree(mfhe_comm* comm, int local_rc, hipStream_t s);
 int hip_error(hipError_t e, const char* what);
 int ensure_xy(mfhe_ctx* c);   // XY encoder matrices, built on first use (ctx.cpp)
+int xcc_census(mfhe_ctx* c);  // fused NTT: XCC id -> queue map (ntt.hip), run when MFHE_OPT_NTT_FUSED is set
 
 #define MFHE_HIP(call)                                          \
     do {                                                        \

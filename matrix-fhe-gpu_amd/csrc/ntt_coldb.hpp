@@ -63,11 +63,68 @@ __device__ __forceinline__ void vm_wait() {
 // (exchanges) or is ordered by an explicit vm_wait (DMA'd tiles), so lgkmcnt(0) + s_barrier suffices.
 __device__ __forceinline__ void lds_barrier() { asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory"); }
 
-template <class TS>
-__global__ __launch_bounds__(ColDb::NT, 1) void ntt_col_db_kernel(PassArgs<TS> a) {
+// One column tile whose DMA has landed in buf ([256 rows][NG] row-major): stages 0..7, the exchange in buf itself,
+// then the raw centred intermediate stored to base (plain stores, R per thread).  tw0: tw[1..15] of the limb
+// (shared), tw1: this thread's round-1 twiddles ((16 + tau) << e) + j.
+// TW0 / TW1: anything indexable by [0, 15) -- register arrays (ntt_col_db_kernel) or LDS (ntt_fused_db_kernel).
+template <class TW0, class TW1>
+__device__ __forceinline__ void coldb_tile(uint64_t* buf, uint32_t gl, uint32_t tau, double q, double qinv,
+                                           const TW0& tw0, const TW1& tw1, uint64_t* base, uint32_t off0, int logS) {
     using A = ArithF64;
     using C = ColDb;
     using Gm = C::Gm;
+    uint64_t* my = buf + (size_t)gl * C::GS;
+    const A ar(LimbConst{0, q, qinv, 0});
+    double x[C::R];
+#pragma unroll
+    for (int k = 0; k < C::R; ++k) x[k] = A::from_u64(buf[(size_t)Gm::g_of(0, tau, k) * C::NG + gl]);
+    // round 0: stages 0..3 (register bits 3..0), twiddles shared by the workgroup
+    static_for<0, 4>([&](auto bi) {
+        constexpr int bb = 3 - decltype(bi)::value, e = 3 - bb, half = 1 << bb;
+#pragma unroll
+        for (int k = 0; k < C::R; ++k) {
+            if (k & half) continue;
+            ar.ct(x[k], x[k + half], tw0[(1 << e) - 1 + (k >> (bb + 1))]);
+        }
+    });
+    lds_barrier();
+#pragma unroll
+    for (int k = 0; k < C::R; ++k) my[Gm::pad(Gm::g_of(0, tau, k))] = A::to_raw(x[k]);
+    lds_barrier();
+#pragma unroll
+    for (int k = 0; k < C::R; ++k) x[k] = ar.round_reduce(A::from_raw(my[Gm::pad(Gm::g_of(1, tau, k))]));
+    // round 1: stages 4..7, twiddles per thread
+    static_for<0, 4>([&](auto bi) {
+        constexpr int bb = 3 - decltype(bi)::value, e = 3 - bb, half = 1 << bb;
+#pragma unroll
+        for (int k = 0; k < C::R; ++k) {
+            if (k & half) continue;
+            ar.ct(x[k], x[k + half], tw1[(1 << e) - 1 + (k >> (bb + 1))]);
+        }
+    });
+    // intermediate (raw doubles, centred), the same words NttPass<COLS, OUT_RAW> writes
+#pragma unroll
+    for (int k = 0; k < C::R; ++k)
+        base[off0 | ((uint32_t)Gm::g_of(1, tau, k) << logS)] = A::to_raw(ar.reduce(x[k]));
+}
+
+// a limb's column-pass twiddles into registers (tw0 shared, tw1 per thread), see coldb_tile.  tw0 is the same
+// for every thread: read through the constant address space it is fetched by scalar loads into SGPRs, which
+// count in lgkmcnt, not in the vmcnt the tile waits are counted against, and cost no VGPRs.
+__device__ __forceinline__ void coldb_twiddles(const double* tw, uint32_t tau, double (&tw0)[15], double (&tw1)[15]) {
+    typedef const __attribute__((address_space(4))) double* ctw_t;
+    const ctw_t ctw = (ctw_t)tw;
+#pragma unroll
+    for (int j = 0; j < 15; ++j) tw0[j] = ctw[1 + j];
+#pragma unroll
+    for (int e = 0; e < 4; ++e)
+#pragma unroll
+        for (int j = 0; j < (1 << e); ++j) tw1[(1 << e) - 1 + j] = tw[((16 + tau) << e) + j];
+}
+
+template <class TS>
+__global__ __launch_bounds__(ColDb::NT, 1) void ntt_col_db_kernel(PassArgs<TS> a) {
+    using C = ColDb;
     extern __shared__ __attribute__((aligned(16))) uint64_t lds[];
     const uint32_t t = threadIdx.x, gl = t % C::NG, tau = t / C::NG, w = t >> 6, lane = t & 63;
     const uint32_t nb = a.nblocks;
@@ -97,22 +154,13 @@ __global__ __launch_bounds__(ColDb::NT, 1) void ntt_col_db_kernel(PassArgs<TS> a
             const LimbConst lc = a.limbs[mod];
             q = lc.qf;
             qinv = lc.qinv;
-            const double* tw = a.tw.p + ((size_t)mod << a.logN);
-#pragma unroll
-            for (int j = 0; j < 15; ++j) tw0[j] = tw[1 + j];
-#pragma unroll
-            for (int e = 0; e < 4; ++e)
-#pragma unroll
-                for (int j = 0; j < (1 << e); ++j) tw1[(1 << e) - 1 + j] = tw[((16 + tau) << e) + j];
+            coldb_twiddles(a.tw.p + ((size_t)mod << a.logN), tau, tw0, tw1);
             vm_wait<0>();   // twiddles in registers (also drains tile t's DMA and the previous stores)
             // re-define the twiddle registers by an (empty) asm after the wait: the compiler's own wait tracking
             // would otherwise keep these loads pending into the butterflies and put a vmcnt(0) there, which
             // also waits for the next tile's DMA
 #pragma unroll
-            for (int j = 0; j < 15; ++j) {
-                asm volatile("" : "+v"(tw0[j]));
-                asm volatile("" : "+v"(tw1[j]));
-            }
+            for (int j = 0; j < 15; ++j) asm volatile("" : "+v"(tw1[j]));
         }
         lds_barrier();   // every thread is done with the other buffer (previous tile's exchange reads)
         uint64_t* nbase = base;
@@ -137,40 +185,7 @@ __global__ __launch_bounds__(ColDb::NT, 1) void ntt_col_db_kernel(PassArgs<TS> a
         lds_barrier();   // ... and every other thread's part
         first = false;
 
-        uint64_t* buf = lds + (size_t)cur * C::BUF;
-        uint64_t* my = buf + (size_t)gl * C::GS;
-        const A ar(LimbConst{0, q, qinv, 0});
-        double x[C::R];
-#pragma unroll
-        for (int k = 0; k < C::R; ++k) x[k] = A::from_u64(buf[(size_t)Gm::g_of(0, tau, k) * C::NG + gl]);
-        // round 0: stages 0..3 (register bits 3..0), twiddles shared by the workgroup
-        static_for<0, 4>([&](auto bi) {
-            constexpr int bb = 3 - decltype(bi)::value, e = 3 - bb, half = 1 << bb;
-#pragma unroll
-            for (int k = 0; k < C::R; ++k) {
-                if (k & half) continue;
-                ar.ct(x[k], x[k + half], tw0[(1 << e) - 1 + (k >> (bb + 1))]);
-            }
-        });
-        lds_barrier();
-#pragma unroll
-        for (int k = 0; k < C::R; ++k) my[Gm::pad(Gm::g_of(0, tau, k))] = A::to_raw(x[k]);
-        lds_barrier();
-#pragma unroll
-        for (int k = 0; k < C::R; ++k) x[k] = ar.round_reduce(A::from_raw(my[Gm::pad(Gm::g_of(1, tau, k))]));
-        // round 1: stages 4..7, twiddles per thread
-        static_for<0, 4>([&](auto bi) {
-            constexpr int bb = 3 - decltype(bi)::value, e = 3 - bb, half = 1 << bb;
-#pragma unroll
-            for (int k = 0; k < C::R; ++k) {
-                if (k & half) continue;
-                ar.ct(x[k], x[k + half], tw1[(1 << e) - 1 + (k >> (bb + 1))]);
-            }
-        });
-        // intermediate (raw doubles, centred), the same words NttPass<COLS, OUT_RAW> writes
-#pragma unroll
-        for (int k = 0; k < C::R; ++k)
-            base[off0 | ((uint32_t)Gm::g_of(1, tau, k) << logS)] = A::to_raw(ar.reduce(x[k]));
+        coldb_tile(lds + (size_t)cur * C::BUF, gl, tau, q, qinv, tw0, tw1, base, off0, logS);
         if (!more) break;
         lt = nlt;
         base = nbase;

@@ -74,7 +74,7 @@ def _run_ntt_config(mfhe, orc, dig, name, arith=0, fused=0, prefetch=None):
     if arith:
         ctx.set_arith(arith)
     if fused:
-        ctx.set_option(OPT_FUSED, 1)
+        ctx.set_option(OPT_FUSED, fused)
     if prefetch is not None:   # default: 2 (DMA-prefetch forward column pass); 0 = the plain column pass
         ctx.set_option(mfhe.OPT_NTT_PREFETCH, prefetch)
     B, nl, st = cfg["batch"], cfg["nl"], cfg["start"]
@@ -98,8 +98,8 @@ def test_c2_full_shape(mfhe, orc, dig):
     _run_ntt_config(mfhe, orc, dig, "c2")
 
 
-@pytest.mark.parametrize("arith,fused,prefetch", [(0, 0, None), (2, 0, None), (0, 1, None), (0, 0, 0)],
-                         ids=["f64", "u64", "f64-fused", "f64-plain-colpass"])
+@pytest.mark.parametrize("arith,fused,prefetch", [(0, 0, None), (2, 0, None), (0, 1, None), (0, 2, None), (0, 0, 0)],
+                         ids=["f64", "u64", "f64-fused", "f64-fused-dma", "f64-plain-colpass"])
 def test_c3_full_shape(mfhe, orc, dig, arith, fused, prefetch):
     _run_ntt_config(mfhe, orc, dig, "c3", arith, fused, prefetch)
 

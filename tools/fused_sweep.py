@@ -32,7 +32,7 @@ def main():
         wgs = [int(x) for x in os.environ.get("FUSED_WGS", "1,2,3,4").split(",")]
         lags = [int(x) for x in os.environ.get("FUSED_LAGS", "1,2,3,4,6,8").split(",")]
         for wg in wgs:
-            for lag in (lags if mode == 1 else (1,)):
+            for lag in (lags if mode >= 1 else (1,)):
                 ctx.set_option(OPT_WG, wg)
                 ctx.set_option(OPT_LAG, lag)
                 ctx.ntt_fwd(d, batch=batch)
