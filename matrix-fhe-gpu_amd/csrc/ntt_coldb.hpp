@@ -108,6 +108,74 @@ __device__ __forceinline__ void coldb_tile(uint64_t* buf, uint32_t gl, uint32_t 
         base[off0 | ((uint32_t)Gm::g_of(1, tau, k) << logS)] = A::to_raw(ar.reduce(x[k]));
 }
 
+// The inverse column pass (the last 8 GS stages, s = 7..0, of the inverse) on a DMA'd tile of the raw centred
+// intermediate the inverse block pass wrote: NttPass<ArithF64, ..., COLS, INV, IN_RAW, !OUT_RAW>'s schedule --
+// round 1 first (register bits 0..3, per-thread twiddles, even executed stage lazy), the exchange, round 0 (shared
+// twiddles; the s = 0 stage folds n^-1 into X), canonical output stored sc1 nt (R buffer stores per thread).
+// The inverse table has the forward one's shape, so tw0 / tw1 are coldb_twiddles of itw: round-1 stage bb uses
+// itw[2^(7-bb) + (tau << (3-bb)) + m] = tw1[2^e - 1 + m], round-0 stage bb uses itw[2^(3-bb) + m] = tw0[2^e - 2 + m + 1]
+// with e = 3 - bb.
+template <class TW0, class TW1>
+__device__ __forceinline__ void coldb_tile_inv(uint64_t* buf, uint32_t gl, uint32_t tau, double q, double qinv,
+                                               double ninv, const TW0& tw0, const TW1& tw1, uint64_t* base,
+                                               uint32_t off0, int logS) {
+    using A = ArithF64;
+    using C = ColDb;
+    using Gm = C::Gm;
+    uint64_t* my = buf + (size_t)gl * C::GS;
+    const A ar(LimbConst{0, q, qinv, 0});
+    double x[C::R];
+#pragma unroll
+    for (int k = 0; k < C::R; ++k) x[k] = A::from_raw(buf[(size_t)Gm::g_of(1, tau, k) * C::NG + gl]);
+    // round 1: stages 7..4 (register bits 0..3); executed stages 0..3 of the pass: even -> lazy GS
+    static_for<0, 4>([&](auto bi) {
+        constexpr int bb = decltype(bi)::value, e = 3 - bb, half = 1 << bb;
+#pragma unroll
+        for (int k = 0; k < C::R; ++k) {
+            if (k & half) continue;
+            const double w = tw1[(1 << e) - 1 + (k >> (bb + 1))];
+            if constexpr (bb % 2 == 0) ar.gs_lazy(x[k], x[k + half], w);
+            else ar.gs(x[k], x[k + half], w);
+        }
+    });
+    lds_barrier();
+#pragma unroll
+    for (int k = 0; k < C::R; ++k) my[Gm::pad(Gm::g_of(1, tau, k))] = A::to_raw(x[k]);
+    lds_barrier();
+#pragma unroll
+    for (int k = 0; k < C::R; ++k) x[k] = A::from_raw(my[Gm::pad(Gm::g_of(0, tau, k))]);
+    // round 0: stages 3..0 (register bits 0..3); executed stages 4..7 of the pass: 4, 6 lazy, 5 reducing, and the
+    // s = 0 stage: X = (u + v) n^-1, Y = (u - v) itw[1] (itw[1] carries n^-1)
+    static_for<0, 4>([&](auto bi) {
+        constexpr int bb = decltype(bi)::value, e = 3 - bb, half = 1 << bb;
+        if constexpr (bb == 3) {
+            const double w1 = tw0[0];
+#pragma unroll
+            for (int k = 0; k < C::R; ++k) {
+                if (k & half) continue;
+                double u = x[k], v = x[k + half];
+                ar.gs_lazy(u, v, w1);
+                x[k] = ar.mulmod(u, ninv);
+                x[k + half] = v;
+            }
+        } else {
+#pragma unroll
+            for (int k = 0; k < C::R; ++k) {
+                if (k & half) continue;
+                const double w = tw0[(1 << e) - 1 + (k >> (bb + 1))];
+                if constexpr (bb % 2 == 0) ar.gs_lazy(x[k], x[k + half], w);
+                else ar.gs(x[k], x[k + half], w);
+            }
+        }
+    });
+    const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(base, 0, 0x7FFFFFFF, 0x00020000);
+#pragma unroll
+    for (int k = 0; k < C::R; ++k)
+        __builtin_amdgcn_raw_buffer_store_b64(
+            __builtin_bit_cast(__attribute__((ext_vector_type(2))) unsigned, ar.canon(x[k])), rs,
+            (int)((off0 | ((uint32_t)Gm::g_of(0, tau, k) << logS)) * 8u), 0, MFHE_NTT_CPOL_OUT);
+}
+
 // a limb's column-pass twiddles into registers (tw0 shared, tw1 per thread), see coldb_tile.  tw0 is the same
 // for every thread: read through the constant address space it is fetched by scalar loads into SGPRs, which
 // count in lgkmcnt, not in the vmcnt the tile waits are counted against, and cost no VGPRs.
@@ -122,7 +190,9 @@ __device__ __forceinline__ void coldb_twiddles(const double* tw, uint32_t tau, d
         for (int j = 0; j < (1 << e); ++j) tw1[(1 << e) - 1 + j] = tw[((16 + tau) << e) + j];
 }
 
-template <class TS>
+// INV: the inverse's last pass (the column stages), reading the raw intermediate of the inverse block pass from
+// the Infinity Cache; otherwise the forward's first pass reading the transform input.
+template <class TS, bool INV = false>
 __global__ __launch_bounds__(ColDb::NT, 1) void ntt_col_db_kernel(PassArgs<TS> a) {
     using C = ColDb;
     extern __shared__ __attribute__((aligned(16))) uint64_t lds[];
@@ -144,7 +214,7 @@ __global__ __launch_bounds__(ColDb::NT, 1) void ntt_col_db_kernel(PassArgs<TS> a
     coldb_dma(tile_ptr(L0), row_bytes, lds, w, lane);
     int cur = 0, mod = -1;
     bool first = true;
-    double q = 0.0, qinv = 0.0;
+    double q = 0.0, qinv = 0.0, ninv = 0.0;
     double tw0[15], tw1[15];   // round 0: tw[1..15] (shared); round 1: ((16 + tau) << e) + j, e = 3 - bb
     while (true) {
         const uint32_t nlt = lt + gridDim.x;
@@ -154,6 +224,7 @@ __global__ __launch_bounds__(ColDb::NT, 1) void ntt_col_db_kernel(PassArgs<TS> a
             const LimbConst lc = a.limbs[mod];
             q = lc.qf;
             qinv = lc.qinv;
+            if constexpr (INV) ninv = a.ninv.p[mod];
             coldb_twiddles(a.tw.p + ((size_t)mod << a.logN), tau, tw0, tw1);
             vm_wait<0>();   // twiddles in registers (also drains tile t's DMA and the previous stores)
             // re-define the twiddle registers by an (empty) asm after the wait: the compiler's own wait tracking
@@ -185,7 +256,8 @@ __global__ __launch_bounds__(ColDb::NT, 1) void ntt_col_db_kernel(PassArgs<TS> a
         lds_barrier();   // ... and every other thread's part
         first = false;
 
-        coldb_tile(lds + (size_t)cur * C::BUF, gl, tau, q, qinv, tw0, tw1, base, off0, logS);
+        if constexpr (INV) coldb_tile_inv(lds + (size_t)cur * C::BUF, gl, tau, q, qinv, ninv, tw0, tw1, base, off0, logS);
+        else coldb_tile(lds + (size_t)cur * C::BUF, gl, tau, q, qinv, tw0, tw1, base, off0, logS);
         if (!more) break;
         lt = nlt;
         base = nbase;

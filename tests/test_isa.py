@@ -46,19 +46,31 @@ def _kernel_asm(symbol_re: str) -> str:
     pytest.fail(f"kernel {symbol_re} not found in {LIB}")
 
 
-def test_column_pass_dma_waits_match_the_instruction_mix():
-    asm = _kernel_asm(r"_ZN4mfhe17ntt_col_db_kernel[^>]*")
+@pytest.mark.parametrize("inv", [False, True], ids=["forward-first-pass", "inverse-last-pass"])
+def test_column_pass_dma_waits_match_the_instruction_mix(inv):
+    asm = _kernel_asm(r"_ZN4mfhe17ntt_col_db_kernelINS_6TwSrcFELb" + ("1" if inv else "0") + r"E[^>]*")
     ops = collections.Counter(re.findall(r"^\s+((?:global|buffer|flat|scratch)_[a-z0-9_]+)", asm, re.M))
     waits = sorted({int(v) for v in re.findall(r"s_waitcnt[^\n]*vmcnt\((\d+)\)", asm)})
-    # ColDb: kDmaOps = 8 DMA instructions per tile (prologue + loop body), R = 16 stores of the intermediate
+    # ColDb: kDmaOps = 8 DMA instructions per tile (prologue + loop body), R = 16 stores per tile: the forward's
+    # intermediate (plain global stores), the inverse's output (sc1 nt buffer stores)
+    store = "buffer_store_dwordx2" if inv else "global_store_dwordx2"
     assert ops["global_load_lds_dwordx4"] == 16, ops
-    assert ops["global_store_dwordx2"] == 16, ops
+    assert ops[store] == 16, ops
     assert not any(k.startswith("scratch_") for k in ops), ops            # no spills
-    assert not any("store" in k for k in ops if k != "global_store_dwordx2"), ops
+    assert not any("store" in k for k in ops if k != store), ops
     # everything else is the once-per-limb twiddle / constant fetch, followed by vmcnt(0)
-    other = {k: v for k, v in ops.items() if k not in ("global_load_lds_dwordx4", "global_store_dwordx2")}
+    other = {k: v for k, v in ops.items() if k not in ("global_load_lds_dwordx4", store)}
     assert set(other) <= {"global_load_dwordx4", "global_load_dwordx2", "global_load_dword"}, ops
     assert sum(other.values()) <= 24, ops
     # the counted waits: 8 (first tile behind the next DMA), 16 (last tile behind the stores), 24 (both)
     assert set(waits) <= {0, 8, 16, 24}, waits
     assert {8, 16, 24} <= set(waits), waits
+
+
+def test_fused_dma_kernel_has_no_spills_and_one_prefetch_wait():
+    """ntt_fused_db_kernel (MFHE_OPT_NTT_FUSED = 2): no scratch, and the only non-zero vmcnt wait is the vmcnt(8)
+    that leaves the next tile's 8 DMA instructions in flight."""
+    asm = _kernel_asm(r"_ZN4mfhe19ntt_fused_db_kernel[^>]*")
+    assert "scratch_" not in asm
+    waits = {int(v) for v in re.findall(r"s_waitcnt[^\n]*vmcnt\((\d+)\)", asm)}
+    assert waits == {0, 8}, waits

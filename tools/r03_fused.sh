@@ -7,12 +7,9 @@ ROOT=${GRAFT_REPO_ROOT:-$(pwd)}
 OUT=$ROOT/gpurun_out/$TAG
 mkdir -p "$OUT"
 cd "$ROOT"
-timeout -k 10 300 python -u -m pytest tests/test_ntt_gpu.py -m gpu -x -v -k "fused" --timeout 120 --timeout-method thread \
-    > "$OUT/pytest_fused.log" 2>&1 || { echo "fused tests failed rc=$?"; tail -30 "$OUT/pytest_fused.log"; exit 2; }
-tail -3 "$OUT/pytest_fused.log"
-timeout -k 10 300 python -u -m pytest tests/test_fullshape_gpu.py -m gpu -x -v -k "c3_full_shape" --timeout 200 \
-    --timeout-method thread > "$OUT/pytest_c3.log" 2>&1 || { echo "c3 full shape failed rc=$?"; tail -30 "$OUT/pytest_c3.log"; exit 3; }
-tail -3 "$OUT/pytest_c3.log"
+timeout -k 10 600 python -u -m pytest tests -m gpu -x -v --timeout 300 --timeout-method thread \
+    > "$OUT/pytest_gpu.log" 2>&1 || { echo "gpu tests failed rc=$?"; tail -30 "$OUT/pytest_gpu.log"; exit 2; }
+tail -3 "$OUT/pytest_gpu.log"
 FUSED_MODE=2 FUSED_WGS=1,2 FUSED_LAGS=2,3,4,6,8,12 timeout -k 10 300 python tools/fused_sweep.py 16,8,1024 \
     > "$OUT/sweep2.txt" 2>&1 || { echo "sweep failed rc=$?"; tail -5 "$OUT/sweep2.txt"; exit 4; }
 cat "$OUT/sweep2.txt"
