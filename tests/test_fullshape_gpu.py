@@ -64,7 +64,7 @@ def _check(got, want, what):
                         f"vs {F.top_digest(want)})"
 
 
-def _run_ntt_config(mfhe, orc, dig, name, arith=0, fused=0, prefetch=None):
+def _run_ntt_config(mfhe, orc, dig, name, arith=0, fused=0, prefetch=None, lag=None):
     import torch
     cfg = F.NTT_CONFIGS[name]
     N = 1 << cfg["log_n"]
@@ -75,6 +75,8 @@ def _run_ntt_config(mfhe, orc, dig, name, arith=0, fused=0, prefetch=None):
         ctx.set_arith(arith)
     if fused:
         ctx.set_option(OPT_FUSED, fused)
+    if lag is not None:
+        ctx.set_option(mfhe.OPT_NTT_FUSED_LAG, lag)
     if prefetch is not None:   # default: 2 (DMA-prefetch forward column pass); 0 = the plain column pass
         ctx.set_option(mfhe.OPT_NTT_PREFETCH, prefetch)
     B, nl, st = cfg["batch"], cfg["nl"], cfg["start"]
@@ -149,3 +151,10 @@ def test_c3_encode_ntt_intt_decode_full_shape(mfhe, orc, dig):
            "C3 wide CRT compose (uniform residues, full path)")
     del res, mag, neg
     torch.cuda.empty_cache()
+
+
+@pytest.mark.parametrize("fused,lag", [(1, 8), (1, 12), (2, 8), (2, 12)])
+def test_c3_full_shape_fused_long_lag(mfhe, orc, dig, fused, lag):
+    """The fused plans at the C3 shape with a long pass-2 lag (more polynomials' intermediates in flight per XCD
+    than its L2 holds)."""
+    _run_ntt_config(mfhe, orc, dig, "c3", 0, fused, None, lag)
