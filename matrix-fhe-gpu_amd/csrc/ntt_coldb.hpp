@@ -34,6 +34,7 @@ struct ColDb {
     static constexpr int NT = NG * TG;                 // 256 threads
     static constexpr int BUF = NG * GS;                // u64 words per tile buffer (exchange layout, 34,944 B)
     static constexpr size_t LDS_BYTES = 2 * (size_t)BUF * sizeof(uint64_t);
+    static constexpr size_t LDS_BYTES_U64 = LDS_BYTES + 512 * sizeof(uint64_t);   // + the U64 twiddle table
     static constexpr int kDmaOps = 256 * NG * 8 / (NT * 16);  // 16-B DMA instructions per thread per tile (8)
     static_assert(Gm::NR == 2 && TG == 16, "two rounds of four stages");
     static_assert(NG == 16 || NG == 32, "16 or 32 columns per tile");
@@ -64,18 +65,17 @@ __device__ __forceinline__ void vm_wait() {
 __device__ __forceinline__ void lds_barrier() { asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory"); }
 
 // One column tile whose DMA has landed in buf ([256 rows][NG] row-major): stages 0..7, the exchange in buf itself,
-// then the raw centred intermediate stored to base (plain stores, R per thread).  tw0: tw[1..15] of the limb
-// (shared), tw1: this thread's round-1 twiddles ((16 + tau) << e) + j.
-// TW0 / TW1: anything indexable by [0, 15) -- register arrays (ntt_col_db_kernel) or LDS (ntt_fused_db_kernel).
-template <class TW0, class TW1>
-__device__ __forceinline__ void coldb_tile(uint64_t* buf, uint32_t gl, uint32_t tau, double q, double qinv,
+// then the raw intermediate (F64: centred doubles; U64: [0, 2q)) stored to base (plain stores, R per thread).
+// tw0: tw[1..15] of the limb (shared), tw1: this thread's round-1 twiddles ((16 + tau) << e) + j.  TW0 / TW1:
+// anything indexable by [0, 15) giving A::Tw -- register arrays (F64), LDS table views (U64, fused kernel).
+template <class A, class TW0, class TW1>
+__device__ __forceinline__ void coldb_tile(uint64_t* buf, uint32_t gl, uint32_t tau, const LimbConst& lc,
                                            const TW0& tw0, const TW1& tw1, uint64_t* base, uint32_t off0, int logS) {
-    using A = ArithF64;
     using C = ColDb;
     using Gm = C::Gm;
     uint64_t* my = buf + (size_t)gl * C::GS;
-    const A ar(LimbConst{0, q, qinv, 0});
-    double x[C::R];
+    const A ar(lc);
+    typename A::T x[C::R];
 #pragma unroll
     for (int k = 0; k < C::R; ++k) x[k] = A::from_u64(buf[(size_t)Gm::g_of(0, tau, k) * C::NG + gl]);
     // round 0: stages 0..3 (register bits 3..0), twiddles shared by the workgroup
@@ -102,11 +102,28 @@ __device__ __forceinline__ void coldb_tile(uint64_t* buf, uint32_t gl, uint32_t 
             ar.ct(x[k], x[k + half], tw1[(1 << e) - 1 + (k >> (bb + 1))]);
         }
     });
-    // intermediate (raw doubles, centred), the same words NttPass<COLS, OUT_RAW> writes
+    // intermediate, the same words NttPass<COLS, OUT_RAW> writes
 #pragma unroll
     for (int k = 0; k < C::R; ++k)
         base[off0 | ((uint32_t)Gm::g_of(1, tau, k) << logS)] = A::to_raw(ar.reduce(x[k]));
 }
+
+// U64 twiddle views of a limb's table T = tw[0, 256) (value and Shoup companion) held in LDS
+struct Tw0U {
+    const uint64_t* w;
+    const uint64_t* ws;
+    __device__ __forceinline__ ulonglong2 operator[](int j) const { return make_ulonglong2(w[1 + j], ws[1 + j]); }
+};
+struct Tw1U {
+    const uint64_t* w;
+    const uint64_t* ws;
+    uint32_t tau;
+    __device__ __forceinline__ ulonglong2 operator[](int i) const {   // i = 2^e - 1 + j, folded at compile time
+        const int e = i >= 7 ? 3 : i >= 3 ? 2 : i >= 1 ? 1 : 0;
+        const uint32_t t = ((16 + tau) << e) + (uint32_t)(i + 1 - (1 << e));
+        return make_ulonglong2(w[t], ws[t]);
+    }
+};
 
 // The inverse column pass (the last 8 GS stages, s = 7..0, of the inverse) on a DMA'd tile of the raw centred
 // intermediate the inverse block pass wrote: NttPass<ArithF64, ..., COLS, INV, IN_RAW, !OUT_RAW>'s schedule --
@@ -115,16 +132,15 @@ __device__ __forceinline__ void coldb_tile(uint64_t* buf, uint32_t gl, uint32_t 
 // The inverse table has the forward one's shape, so tw0 / tw1 are coldb_twiddles of itw: round-1 stage bb uses
 // itw[2^(7-bb) + (tau << (3-bb)) + m] = tw1[2^e - 1 + m], round-0 stage bb uses itw[2^(3-bb) + m] = tw0[2^e - 2 + m + 1]
 // with e = 3 - bb.
-template <class TW0, class TW1>
-__device__ __forceinline__ void coldb_tile_inv(uint64_t* buf, uint32_t gl, uint32_t tau, double q, double qinv,
-                                               double ninv, const TW0& tw0, const TW1& tw1, uint64_t* base,
+template <class A, class TW0, class TW1>
+__device__ __forceinline__ void coldb_tile_inv(uint64_t* buf, uint32_t gl, uint32_t tau, const LimbConst& lc,
+                                               typename A::Tw ninv, const TW0& tw0, const TW1& tw1, uint64_t* base,
                                                uint32_t off0, int logS) {
-    using A = ArithF64;
     using C = ColDb;
     using Gm = C::Gm;
     uint64_t* my = buf + (size_t)gl * C::GS;
-    const A ar(LimbConst{0, q, qinv, 0});
-    double x[C::R];
+    const A ar(lc);
+    typename A::T x[C::R];
 #pragma unroll
     for (int k = 0; k < C::R; ++k) x[k] = A::from_raw(buf[(size_t)Gm::g_of(1, tau, k) * C::NG + gl]);
     // round 1: stages 7..4 (register bits 0..3); executed stages 0..3 of the pass: even -> lazy GS
@@ -133,7 +149,7 @@ __device__ __forceinline__ void coldb_tile_inv(uint64_t* buf, uint32_t gl, uint3
 #pragma unroll
         for (int k = 0; k < C::R; ++k) {
             if (k & half) continue;
-            const double w = tw1[(1 << e) - 1 + (k >> (bb + 1))];
+            const auto w = tw1[(1 << e) - 1 + (k >> (bb + 1))];
             if constexpr (bb % 2 == 0) ar.gs_lazy(x[k], x[k + half], w);
             else ar.gs(x[k], x[k + half], w);
         }
@@ -149,11 +165,11 @@ __device__ __forceinline__ void coldb_tile_inv(uint64_t* buf, uint32_t gl, uint3
     static_for<0, 4>([&](auto bi) {
         constexpr int bb = decltype(bi)::value, e = 3 - bb, half = 1 << bb;
         if constexpr (bb == 3) {
-            const double w1 = tw0[0];
+            const auto w1 = tw0[0];
 #pragma unroll
             for (int k = 0; k < C::R; ++k) {
                 if (k & half) continue;
-                double u = x[k], v = x[k + half];
+                typename A::T u = x[k], v = x[k + half];
                 ar.gs_lazy(u, v, w1);
                 x[k] = ar.mulmod(u, ninv);
                 x[k + half] = v;
@@ -162,13 +178,17 @@ __device__ __forceinline__ void coldb_tile_inv(uint64_t* buf, uint32_t gl, uint3
 #pragma unroll
             for (int k = 0; k < C::R; ++k) {
                 if (k & half) continue;
-                const double w = tw0[(1 << e) - 1 + (k >> (bb + 1))];
+                const auto w = tw0[(1 << e) - 1 + (k >> (bb + 1))];
                 if constexpr (bb % 2 == 0) ar.gs_lazy(x[k], x[k + half], w);
                 else ar.gs(x[k], x[k + half], w);
             }
         }
     });
-    const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(base, 0, 0x7FFFFFFF, 0x00020000);
+    // base is workgroup-uniform; say so (the U64 kernel otherwise wraps every store in a readfirstlane loop)
+    const uint64_t bu = (uint64_t)base;
+    uint64_t* const ubase = (uint64_t*)(((uint64_t)(uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)(bu >> 32)) << 32) |
+                                        (uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)bu));
+    const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(ubase, 0, 0x7FFFFFFF, 0x00020000);
 #pragma unroll
     for (int k = 0; k < C::R; ++k)
         __builtin_amdgcn_raw_buffer_store_b64(
@@ -192,9 +212,13 @@ __device__ __forceinline__ void coldb_twiddles(const double* tw, uint32_t tau, d
 
 // INV: the inverse's last pass (the column stages), reading the raw intermediate of the inverse block pass from
 // the Infinity Cache; otherwise the forward's first pass reading the transform input.
-template <class TS, bool INV = false>
+// A = ArithF64: the limb's twiddles in registers (tw0 by scalar loads); A = ArithU64: the limb's table tw[0, 256)
+// and its Shoup companions DMA'd into LDS (4 KiB after the two tile buffers) -- 30 (w, w') pairs per thread do
+// not fit beside the U64 butterflies' registers, and per-butterfly global loads were the r02 U64 pass's stall.
+template <class A, class TS, bool INV = false>
 __global__ __launch_bounds__(ColDb::NT, 1) void ntt_col_db_kernel(PassArgs<TS> a) {
     using C = ColDb;
+    constexpr bool U = std::is_same<A, ArithU64>::value;
     extern __shared__ __attribute__((aligned(16))) uint64_t lds[];
     const uint32_t t = threadIdx.x, gl = t % C::NG, tau = t / C::NG, w = t >> 6, lane = t & 63;
     const uint32_t nb = a.nblocks;
@@ -206,6 +230,8 @@ __global__ __launch_bounds__(ColDb::NT, 1) void ntt_col_db_kernel(PassArgs<TS> a
         return tile_loc<C::LOG_G, C::NG, true, true>(a.data, a.batch, a.nl, a.start_limb, a.logN, 0, xcd_remap(l, nb), gl);
     };
     auto tile_ptr = [&](const TileLoc& L) { return (const char*)(L.base + (L.off0 - gl)); };
+    uint64_t* tabw = lds + 2 * C::BUF;   // U64: [0, 256) values, [256, 512) Shoup companions
+    typedef __attribute__((address_space(3))) void* lds_vp;
 
     TileLoc L0 = locate(lt);
     uint64_t* base = L0.base;   // current tile: polynomial base, element offset of its first row, limb
@@ -214,24 +240,42 @@ __global__ __launch_bounds__(ColDb::NT, 1) void ntt_col_db_kernel(PassArgs<TS> a
     coldb_dma(tile_ptr(L0), row_bytes, lds, w, lane);
     int cur = 0, mod = -1;
     bool first = true;
-    double q = 0.0, qinv = 0.0, ninv = 0.0;
-    double tw0[15], tw1[15];   // round 0: tw[1..15] (shared); round 1: ((16 + tau) << e) + j, e = 3 - bb
+    LimbConst lc{};
+    typename A::Tw ninv{};
+    double tw0[15], tw1[15];   // F64 round 0: tw[1..15] (shared); round 1: ((16 + tau) << e) + j, e = 3 - bb
     while (true) {
         const uint32_t nlt = lt + gridDim.x;
         const bool more = nlt < nb;   // workgroup-uniform
         if (lmod != mod) {
             mod = lmod;
-            const LimbConst lc = a.limbs[mod];
-            q = lc.qf;
-            qinv = lc.qinv;
-            if constexpr (INV) ninv = a.ninv.p[mod];
-            coldb_twiddles(a.tw.p + ((size_t)mod << a.logN), tau, tw0, tw1);
-            vm_wait<0>();   // twiddles in registers (also drains tile t's DMA and the previous stores)
-            // re-define the twiddle registers by an (empty) asm after the wait: the compiler's own wait tracking
-            // would otherwise keep these loads pending into the butterflies and put a vmcnt(0) there, which
-            // also waits for the next tile's DMA
+            // per-limb constants by scalar loads (constant address space): a vector load here would make the
+            // compiler put a vmcnt(0) before their first use in the butterflies, which waits for the prefetch
+            {
+                const __attribute__((address_space(4))) LimbConst* cl =
+                    (const __attribute__((address_space(4))) LimbConst*)a.limbs + mod;
+                lc.q = cl->q;
+                lc.qf = cl->qf;
+                lc.qinv = cl->qinv;
+            }
+            if constexpr (!U) {
+                if constexpr (INV) ninv = ((const __attribute__((address_space(4))) double*)a.ninv.p)[mod];
+                coldb_twiddles(a.tw.p + ((size_t)mod << a.logN), tau, tw0, tw1);
+                vm_wait<0>();   // twiddles in registers (also drains tile t's DMA and the previous stores)
+                // re-define the twiddle registers by an (empty) asm after the wait: the compiler's own wait tracking
+                // would otherwise keep these loads pending into the butterflies and put a vmcnt(0) there, which
+                // also waits for the next tile's DMA
 #pragma unroll
-            for (int j = 0; j < 15; ++j) asm volatile("" : "+v"(tw1[j]));
+                for (int j = 0; j < 15; ++j) asm volatile("" : "+v"(tw1[j]));
+            } else {
+                typedef const __attribute__((address_space(4))) uint64_t* cu64_t;
+                if constexpr (INV) ninv = make_ulonglong2(((cu64_t)a.ninv.w)[mod], ((cu64_t)a.ninv.ws)[mod]);
+                lds_barrier();   // every thread is done with the previous limb's table
+                // waves 0, 1: tw[0, 256); waves 2, 3: the Shoup companions (1 KiB per DMA instruction)
+                const uint64_t* src = (w < 2 ? a.tw.w : a.tw.ws) + ((size_t)mod << a.logN) + (w & 1) * 128 + lane * 2;
+                __builtin_amdgcn_global_load_lds((const void*)src, (lds_vp)(tabw + (w >> 1) * 256 + (w & 1) * 128), 16,
+                                                 0, 0);
+                vm_wait<0>();   // table landed for this wave (published by the barrier below)
+            }
         }
         lds_barrier();   // every thread is done with the other buffer (previous tile's exchange reads)
         uint64_t* nbase = base;
@@ -256,8 +300,16 @@ __global__ __launch_bounds__(ColDb::NT, 1) void ntt_col_db_kernel(PassArgs<TS> a
         lds_barrier();   // ... and every other thread's part
         first = false;
 
-        if constexpr (INV) coldb_tile_inv(lds + (size_t)cur * C::BUF, gl, tau, q, qinv, ninv, tw0, tw1, base, off0, logS);
-        else coldb_tile(lds + (size_t)cur * C::BUF, gl, tau, q, qinv, tw0, tw1, base, off0, logS);
+        uint64_t* buf = lds + (size_t)cur * C::BUF;
+        if constexpr (U) {
+            const Tw0U t0{tabw, tabw + 256};
+            const Tw1U t1{tabw, tabw + 256, tau};
+            if constexpr (INV) coldb_tile_inv<A>(buf, gl, tau, lc, ninv, t0, t1, base, off0, logS);
+            else coldb_tile<A>(buf, gl, tau, lc, t0, t1, base, off0, logS);
+        } else {
+            if constexpr (INV) coldb_tile_inv<A>(buf, gl, tau, lc, ninv, tw0, tw1, base, off0, logS);
+            else coldb_tile<A>(buf, gl, tau, lc, tw0, tw1, base, off0, logS);
+        }
         if (!more) break;
         lt = nlt;
         base = nbase;

@@ -61,6 +61,9 @@ __global__ __launch_bounds__(FusedDb::NT, 2) void ntt_fused_db_kernel(FusedArgs<
     FusedSync* sy = f.sync;
     const uint32_t K = C::K, D = f.lag, Q = f.nq;
     constexpr uint32_t kNone = 0xFFFFFFFFu;
+    // outputs stored nt (streaming, write-back): the lines they overwrite hold this launch's intermediate, dirty in
+    // the XCD's L2; an sc1 store (write-through, drops the line) over a dirty line is not used here
+    constexpr int kCpolOut = 2;
     // per-limb constants through the constant address space: scalar loads (lgkmcnt), which neither count
     // against the vmcnt waits nor make the compiler wait on vmcnt before their first use
     typedef const __attribute__((address_space(4))) LimbConst* climb_t;
@@ -240,7 +243,7 @@ __global__ __launch_bounds__(FusedDb::NT, 2) void ntt_fused_db_kernel(FusedArgs<
                 for (int k = 0; k < C::R; ++k)
                     __builtin_amdgcn_raw_buffer_store_b64(
                         __builtin_bit_cast(__attribute__((ext_vector_type(2))) unsigned, ar.canon(x[k])), rs,
-                        (int)((Lc.off0 + k * 16 + tau2) * 8u), 0, MFHE_NTT_CPOL_OUT);
+                        (int)((Lc.off0 + k * 16 + tau2) * 8u), 0, kCpolOut);
             } else if (kc_kind == 1) {
                 const TileLoc Lc = loc1(kc, uc);
                 if (Lc.mod != lmod) {
@@ -258,7 +261,7 @@ __global__ __launch_bounds__(FusedDb::NT, 2) void ntt_fused_db_kernel(FusedArgs<
                 issue_next_and_wait(kn_kind, kn, un, nbuf);
                 lds_barrier();   // the tile (and table) landed for every thread
                 signal();        // the previous pass-1 tile's stores were older than the 8 DMAs: complete
-                coldb_tile(buf, gl1, tau1, q1, qi1, tw0, tw1, Lc.base, Lc.off0, 8);
+                coldb_tile<A>(buf, gl1, tau1, LimbConst{0, q1, qi1, 0}, tw0, tw1, Lc.base, Lc.off0, 8);
                 pend = kc;
             } else {
                 issue_next_and_wait(kn_kind, kn, un, nbuf);

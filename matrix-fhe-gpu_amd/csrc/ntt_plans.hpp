@@ -113,12 +113,12 @@ static int launch_pass(const NttJob<TS>& j, int s0, hipStream_t st) {
 // whose kernel spills (scratch loads/stores are vector-memory ops too) would make them too loose.  Checked once
 // per process from the code object's metadata; such a build runs the plain column pass instead
 // (tests/test_isa.py checks the instruction counts of the shipped library).
-template <bool INV>
+template <class A, class TS, bool INV>
 static bool col_db_usable() {
     static int ok = -1;
     if (ok < 0) {
         hipFuncAttributes fa{};
-        ok = hipFuncGetAttributes(&fa, reinterpret_cast<const void*>(ntt_col_db_kernel<TwSrcF, INV>)) == hipSuccess &&
+        ok = hipFuncGetAttributes(&fa, reinterpret_cast<const void*>(ntt_col_db_kernel<A, TS, INV>)) == hipSuccess &&
              fa.localSizeBytes == 0;
     }
     return ok == 1;
@@ -126,15 +126,16 @@ static bool col_db_usable() {
 
 // column pass with the next tile's DMA in flight (ntt_coldb.hpp), MFHE_OPT_NTT_PREFETCH = 2: the forward's first
 // pass, or (INV) the inverse's last pass
-template <bool INV>
-static int launch_col_db(const NttJob<TwSrcF>& j, hipStream_t st) {
+template <class A, class TS, bool INV>
+static int launch_col_db(const NttJob<TS>& j, hipStream_t st) {
     using C = ColDb;
+    constexpr size_t lds = std::is_same<A, ArithU64>::value ? C::LDS_BYTES_U64 : C::LDS_BYTES;
     const uint64_t npl = j.batch * (uint64_t)j.nl;
     const uint64_t nb = npl << (j.logN - C::LOG_G - C::LOG_NG);   // NG-column tiles: 2^(logN - 8) / NG per polynomial
     if (nb == 0) return MFHE_OK;
     if (nb > 0xFFFFFFFFull || npl >= 0xFFFFFFFFull)
         return set_error(MFHE_EINVAL, "NTT batch too large for one launch (batch * nlimbs must be < 2^32)");
-    PassArgs<TwSrcF> a{};
+    PassArgs<TS> a{};
     a.data = j.data;
     a.tw = j.tw;
     a.ninv = j.ninv;
@@ -148,13 +149,15 @@ static int launch_col_db(const NttJob<TwSrcF>& j, hipStream_t st) {
     static int occ = 0;
     if (occ == 0) {
         int o = 0;
-        if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&o, ntt_col_db_kernel<TwSrcF, INV>, C::NT, C::LDS_BYTES) != hipSuccess || o < 1) o = 1;
+        if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&o, ntt_col_db_kernel<A, TS, INV>, C::NT, lds) != hipSuccess ||
+            o < 1)
+            o = 1;
         occ = o;
     }
     const int per_cu = j.wg_per_cu > 0 ? std::min(j.wg_per_cu, occ) : occ;
     const uint64_t cap = std::max<uint64_t>(8, ((uint64_t)per_cu * j.num_cus) & ~7ull);
     const uint32_t grid = (uint32_t)std::min<uint64_t>(nb, cap);
-    hipLaunchKernelGGL((ntt_col_db_kernel<TwSrcF, INV>), dim3(grid), dim3(C::NT), C::LDS_BYTES, st, a);
+    hipLaunchKernelGGL((ntt_col_db_kernel<A, TS, INV>), dim3(grid), dim3(C::NT), lds, st, a);
     MFHE_CHECK_LAUNCH("ntt_col_db_kernel launch");
     return MFHE_OK;
 }
@@ -209,9 +212,10 @@ static int two_pass_chunk(const NttJob<TS>& c, int pass, hipStream_t st) {
             return launch_pass<A, TS, LOG_GB, 4, NGB, false, false, true, false, false, false, true, true>(c, LOG_GA, st);
         }
     }
-    if constexpr (std::is_same<A, ArithF64>::value && LOG_GA == 8 && NGA == 16) {
+    if constexpr (LOG_GA == 8 && NGA == 16) {
         // the column pass with the next tile's DMA in flight: the forward's first pass, the inverse's second
-        if (pass == (INV ? 1 : 0) && c.prefetch == 2 && c.limbs && col_db_usable<INV>()) return launch_col_db<INV>(c, st);
+        if (pass == (INV ? 1 : 0) && c.prefetch == 2 && c.limbs && col_db_usable<A, TS, INV>())
+            return launch_col_db<A, TS, INV>(c, st);
     }
     if (!INV) {
         if (pass == 0) return launch_pass<A, TS, LOG_GA, 4, NGA, true, false, false, true, false, false, true>(c, 0, st);

@@ -46,15 +46,18 @@ def _kernel_asm(symbol_re: str) -> str:
     pytest.fail(f"kernel {symbol_re} not found in {LIB}")
 
 
+@pytest.mark.parametrize("arith", ["F64", "U64"])
 @pytest.mark.parametrize("inv", [False, True], ids=["forward-first-pass", "inverse-last-pass"])
-def test_column_pass_dma_waits_match_the_instruction_mix(inv):
-    asm = _kernel_asm(r"_ZN4mfhe17ntt_col_db_kernelINS_6TwSrcFELb" + ("1" if inv else "0") + r"E[^>]*")
+def test_column_pass_dma_waits_match_the_instruction_mix(inv, arith):
+    asm = _kernel_asm(r"_ZN4mfhe17ntt_col_db_kernelINS_8Arith" + arith + r"ENS_6TwSrc" + arith[0] +
+                      r"ELb" + ("1" if inv else "0") + r"E[^>]*")
     ops = collections.Counter(re.findall(r"^\s+((?:global|buffer|flat|scratch)_[a-z0-9_]+)", asm, re.M))
     waits = sorted({int(v) for v in re.findall(r"s_waitcnt[^\n]*vmcnt\((\d+)\)", asm)})
     # ColDb: kDmaOps = 8 DMA instructions per tile (prologue + loop body), R = 16 stores per tile: the forward's
     # intermediate (plain global stores), the inverse's output (sc1 nt buffer stores)
     store = "buffer_store_dwordx2" if inv else "global_store_dwordx2"
-    assert ops["global_load_lds_dwordx4"] == 16, ops
+    # U64: + 1 DMA instruction per wave for the limb's twiddle table (issued before the limb's vmcnt(0))
+    assert ops["global_load_lds_dwordx4"] == (17 if arith == "U64" else 16), ops
     assert ops[store] == 16, ops
     assert not any(k.startswith("scratch_") for k in ops), ops            # no spills
     assert not any("store" in k for k in ops if k != store), ops
@@ -65,6 +68,16 @@ def test_column_pass_dma_waits_match_the_instruction_mix(inv):
     # the counted waits: 8 (first tile behind the next DMA), 16 (last tile behind the stores), 24 (both)
     assert set(waits) <= {0, 8, 16, 24}, waits
     assert {8, 16, 24} <= set(waits), waits
+    # and no compiler wait inside the butterflies: the tile's butterflies are one straight-line block ending in
+    # its first store (the compiler lays the blocks out in varying order, so walk back from that store to the
+    # previous branch or counted wait); no other vmcnt wait may sit in it (one would wait for the prefetch too)
+    lines = asm.split("\n")
+    s0 = next(i for i, l in enumerate(lines) if re.search(r"\b(global|buffer)_store", l))
+    b0 = max(i for i in range(s0) if re.search(r"\bs_(c?branch|endpgm)|vmcnt\((8|16|24)\)", lines[i]))
+    assert s0 - b0 > 300, (b0, s0)   # the block really holds the butterflies
+    assert not any("vmcnt" in l for l in lines[b0 + 1:s0]), [l for l in lines[b0 + 1:s0] if "vmcnt" in l]
+    # the stores' base is uniform: no readfirstlane (waterfall) loop around them
+    assert "s_cbranch_execnz" not in "\n".join(lines[s0:s0 + 80]), "stores wrapped in a waterfall loop"
 
 
 def test_fused_dma_kernel_has_no_spills_and_one_prefetch_wait():

@@ -4,8 +4,8 @@
 //
 //   A  two passes per chunk with the NTT's own access patterns: a column pass (16-column x 256-row tiles, one
 //      column per lane group, plain loads / plain stores: the intermediate stays in the Infinity Cache) then a
-//      block pass (4 contiguous 256-element rows per 64-thread workgroup, plain loads / sc1 nt stores), each
-//      lane moving 16 words, exactly like ntt_pass_kernel / ntt_col_db_kernel move them
+//      block pass (16 contiguous 256-element rows per workgroup, plain loads / sc1 nt stores), each lane moving
+//      16 words, persistent grids with the XCD-contiguous tile order the NTT uses (no LDS, no DMA)
 //   B  two passes per chunk as contiguous 16-B in-place read-modify-write sweeps (the same bytes, the
 //      friendliest order)
 //   C  one contiguous in-place read-modify-write sweep over the whole 4 GiB (the single-pass floor)
@@ -30,36 +30,42 @@
 constexpr int LOGN = 16, NPOLY = 8192, NCHUNK = 18;
 constexpr uint64_t N = 1ull << LOGN;
 
+// blockIdx -> tile, XCD-aware as the NTT's xcd_remap: workgroups are dispatched round-robin over the 8 XCDs, so
+// logical tile l runs on XCD l % 8; give each XCD a contiguous run of tiles (nb % 8 == 0 here)
+__device__ __forceinline__ uint32_t xcd_tile(uint32_t l, uint32_t nb) { return (l & 7) * (nb >> 3) + (l >> 3); }
+
 // column pass: tile = 16 columns x 256 rows of one polynomial (256 x 256 view), 256 threads: lane group gl =
-// t % 16 (column), tau = t / 16 owns rows tau * 16 + k -- the NTT's round-1 store layout
+// t % 16 (column), tau = t / 16 owns rows tau * 16 + k -- the NTT's round-1 store layout; persistent grid
 __global__ __launch_bounds__(256) void col_pass(uint64_t* d, uint32_t ntiles) {
-    const uint32_t tile = blockIdx.x;
-    if (tile >= ntiles) return;
-    const uint32_t poly = tile >> 4, ct = tile & 15;
     const uint32_t gl = threadIdx.x & 15, tau = threadIdx.x >> 4;
-    uint64_t* base = d + ((uint64_t)poly << LOGN) + ct * 16 + gl;
-    uint64_t x[16];
+    for (uint32_t l = blockIdx.x; l < ntiles; l += gridDim.x) {
+        const uint32_t tile = xcd_tile(l, ntiles);
+        const uint32_t poly = tile >> 4, ct = tile & 15;
+        uint64_t* base = d + ((uint64_t)poly << LOGN) + ct * 16 + gl;
+        uint64_t x[16];
 #pragma unroll
-    for (int k = 0; k < 16; ++k) x[k] = base[(uint64_t)(tau * 16 + k) << 8];
+        for (int k = 0; k < 16; ++k) x[k] = base[(uint64_t)(tau * 16 + k) << 8];
 #pragma unroll
-    for (int k = 0; k < 16; ++k) base[(uint64_t)(tau * 16 + k) << 8] = x[k] + 1;
+        for (int k = 0; k < 16; ++k) base[(uint64_t)(tau * 16 + k) << 8] = x[k] + 1;
+    }
 }
 
-// block pass: 4 contiguous 256-element rows per 64-thread workgroup, element k * 16 + tau of row gl, outputs
-// stored sc1 nt as the NTT's final stores
-__global__ __launch_bounds__(64) void blk_pass(uint64_t* d, uint32_t ntiles) {
-    const uint32_t tile = blockIdx.x;
-    if (tile >= ntiles) return;
+// block pass: 16 contiguous 256-element rows per 256-thread workgroup (4 per wave), element k * 16 + tau of row
+// gl, outputs stored sc1 nt as the NTT's final stores; persistent grid
+__global__ __launch_bounds__(256) void blk_pass(uint64_t* d, uint32_t ntiles) {
     const uint32_t gl = threadIdx.x >> 4, tau = threadIdx.x & 15;
-    uint64_t* row = d + ((uint64_t)tile * 4 + gl) * 256 + tau;
-    const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(row, 0, 0x7FFFFFFF, 0x00020000);
-    uint64_t x[16];
+    for (uint32_t l = blockIdx.x; l < ntiles; l += gridDim.x) {
+        const uint32_t tile = xcd_tile(l, ntiles);
+        uint64_t* row = d + ((uint64_t)tile * 16 + gl) * 256 + tau;
+        const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(row, 0, 0x7FFFFFFF, 0x00020000);
+        uint64_t x[16];
 #pragma unroll
-    for (int k = 0; k < 16; ++k) x[k] = row[k * 16];
+        for (int k = 0; k < 16; ++k) x[k] = row[k * 16];
 #pragma unroll
-    for (int k = 0; k < 16; ++k)
-        __builtin_amdgcn_raw_buffer_store_b64(__builtin_bit_cast(__attribute__((ext_vector_type(2))) unsigned, x[k] ^ 3),
-                                              rs, k * 16 * 8, 0, 18);
+        for (int k = 0; k < 16; ++k)
+            __builtin_amdgcn_raw_buffer_store_b64(
+                __builtin_bit_cast(__attribute__((ext_vector_type(2))) unsigned, x[k] ^ 3), rs, k * 16 * 8, 0, 18);
+    }
 }
 
 // contiguous in-place read-modify-write, 16 B per lane, grid-stride
@@ -91,8 +97,8 @@ int main() {
     auto variant_a = [&]() {
         for (uint32_t p0 = 0; p0 < NPOLY; p0 += cb) {
             const uint32_t np = p0 + cb <= NPOLY ? cb : NPOLY - p0;
-            hipLaunchKernelGGL(col_pass, dim3(np * 16), dim3(256), 0, 0, d + (uint64_t)p0 * N, np * 16);
-            hipLaunchKernelGGL(blk_pass, dim3(np * 64), dim3(64), 0, 0, d + (uint64_t)p0 * N, np * 64);
+            hipLaunchKernelGGL(col_pass, dim3(512), dim3(256), 0, 0, d + (uint64_t)p0 * N, np * 16);
+            hipLaunchKernelGGL(blk_pass, dim3(2048), dim3(256), 0, 0, d + (uint64_t)p0 * N, np * 16);
         }
     };
     auto variant_b = [&]() {
