@@ -568,7 +568,7 @@ extern "C" int mfhe_ctx_set_option(mfhe_ctx* c, int opt, int64_t v) {
             c->ntt_pack = (int)v;
             return MFHE_OK;
         case MFHE_OPT_NTT_FUSED:
-            if (v < 0 || v > 2) return set_error(MFHE_EINVAL, "fused must be 0, 1 or 2");
+            if (v < 0 || v > 1) return set_error(MFHE_EINVAL, "fused must be 0 or 1");
             if (v) {
                 int dev = 0;
                 if (hipGetDevice(&dev) == hipSuccess && dev != c->device)
@@ -584,6 +584,10 @@ extern "C" int mfhe_ctx_set_option(mfhe_ctx* c, int opt, int64_t v) {
         case MFHE_OPT_WCRT_MFMA:
             if (v < 0 || v > 3) return set_error(MFHE_EINVAL, "wcrt mfma must be 0, 1, 2 or 3");
             c->wcrt_mfma = (int)v;
+            return MFHE_OK;
+        case MFHE_OPT_WCRT_PIPE:
+            if (v < 0 || v > 2) return set_error(MFHE_EINVAL, "wcrt pipe must be 0, 1 or 2");
+            c->wcrt_pipe = (int)v;
             return MFHE_OK;
         case MFHE_OPT_CGEMM_MFMA:
             if (v < 0 || v > 1) return set_error(MFHE_EINVAL, "cgemm mfma must be 0 or 1");
@@ -633,6 +637,7 @@ extern "C" int mfhe_ctx_get_option(const mfhe_ctx* c, int opt, int64_t* v) {
         case MFHE_OPT_NTT_PREFETCH: *v = c->ntt_prefetch; return MFHE_OK;
         case MFHE_OPT_NTT_FUSED: *v = c->ntt_fused; return MFHE_OK;
         case MFHE_OPT_NTT_PACK: *v = c->ntt_pack; return MFHE_OK;
+        case MFHE_OPT_WCRT_PIPE: *v = c->wcrt_pipe; return MFHE_OK;
         case MFHE_OPT_WCRT_MFMA: *v = c->d_wVdig ? c->wcrt_mfma : 0; return MFHE_OK;
         case MFHE_OPT_CGEMM_MFMA: *v = c->cgemm_mfma; return MFHE_OK;
         case MFHE_OPT_HE_FUSED: *v = c->he_fused; return MFHE_OK;

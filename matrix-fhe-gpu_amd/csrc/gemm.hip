@@ -583,6 +583,94 @@ __global__ __launch_bounds__(256, D <= 5 ? 2 : 1) void mod_gemm_mfma_lds_kernel(
     mfma_epilogue<D, FAC>(a, acc, l, mb + wm, (uint32_t)(pb + wp), r, h, Ppad);
 }
 
+// Ring variant (MFHE_OPT_WCRT_PIPE >= 1): the same tile, digit planes and epilogue, but the K loop runs over
+// 32-k stages (one panel per digit plane per operand, 4 D KiB) held in a 4-slot LDS ring (80 KiB at D = 5: still
+// 2 workgroups per CU).  Stage s + 3 is DMA'd while stage s is multiplied, so a stage's bytes have three stage
+// times to land instead of one, and the wait at the end of stage s is a counted vmcnt that leaves stages s + 2
+// and s + 3 in flight (D DMA instructions per thread per stage; nothing else in the loop touches vector memory).
+// The barrier after it is a raw s_barrier (__syncthreads' fence would wait for the DMAs in flight).  Slot
+// (s + 3) & 3 = (s - 1) & 3 was last read in stage s - 1, which every wave has left at that barrier.
+// AHEAD: the next A fragment's LDS read is issued before the current fragment's D MFMAs (sched_barrier-pinned),
+// so its latency hides behind them instead of being waited for in front of them (D <= 5 only: at D >= 6 the
+// extra fragment spills).
+template <int D, bool FAC, bool AHEAD>
+__global__ __launch_bounds__(256, D <= 5 ? 2 : 1) void mod_gemm_mfma_ring_kernel(ModGemmArgs a, uint32_t Ppad, int limb0) {
+    constexpr int KK = FAC ? FK : MK, AM = FAC ? FK : 512;
+    const uint32_t Pcols = FAC ? 2 * Ppad : Ppad;
+    constexpr int NS = 2 * D - 1;
+    constexpr int NST = KK / 32;                 // 32-k stages
+    constexpr int PANEL = 64 * 32;               // 64 rows x 32 k of one digit plane (bytes)
+    constexpr int STAGE = 2 * D * PANEL;         // A planes then B planes
+    constexpr int NSLOT = 4;
+    static_assert(NST >= NSLOT, "ring prologue assumes at least 4 stages");
+    __shared__ __attribute__((aligned(16))) int8_t lds[NSLOT * STAGE];
+    const int l = limb0 + blockIdx.z;
+    const int t = threadIdx.x, lane = t & 63, w = t >> 6;
+    const int r = lane & 31, h = lane >> 5;
+    const int mb = blockIdx.y * 64, pb = blockIdx.x * 64;
+    const int wm = (w & 1) * 32, wp = (w >> 1) * 32;
+    const bool ldA = t < 128;
+    const int li = t & 127;
+    const uint64_t rows = ldA ? AM : Pcols;
+    const int8_t* src = (ldA ? a.Adig + (uint64_t)l * a.adL : a.Bdig + (uint64_t)l * a.D * Pcols * KK) +
+                        (uint64_t)(ldA ? mb : pb) * 32 + li * 16;
+    const uint64_t pstride = rows * KK, kstride = rows * 32;
+    const int wbase = (ldA ? 0 : D * PANEL) + (li & ~63) * 16;
+    auto issue = [&](int s) {
+        int8_t* dst = lds + (s & (NSLOT - 1)) * STAGE + wbase;
+#pragma unroll
+        for (int i = 0; i < D; ++i)
+            __builtin_amdgcn_global_load_lds((const void*)(src + i * pstride + (uint64_t)s * kstride),
+                                             (lds_ptr_t)(dst + i * PANEL), 16, 0, 0);
+    };
+    auto barrier = []() { asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory"); };
+    v16i acc[NS];
+#pragma unroll
+    for (int s = 0; s < NS; ++s) acc[s] = v16i{0};
+    issue(0);
+    issue(1);
+    issue(2);
+    asm volatile("s_waitcnt vmcnt(%0)" ::"n"(2 * D) : "memory");   // stage 0 landed (1 and 2 in flight)
+    barrier();
+    for (int s = 0; s < NST; ++s) {
+        if (s + 3 < NST) issue(s + 3);
+        const int8_t* st = lds + (s & (NSLOT - 1)) * STAGE;
+        v4i bv[D];
+#pragma unroll
+        for (int j = 0; j < D; ++j) bv[j] = *(const v4i*)(st + (D + j) * PANEL + (wp + r) * 32 + 16 * h);
+        if constexpr (AHEAD) {
+            v4i an = *(const v4i*)(st + (wm + r) * 32 + 16 * h);
+#pragma unroll
+            for (int i = 0; i < D; ++i) {
+                const v4i av = an;
+                if (i + 1 < D) an = *(const v4i*)(st + (i + 1) * PANEL + (wm + r) * 32 + 16 * h);
+                __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+                for (int j = 0; j < D; ++j)
+                    acc[i + j] = __builtin_amdgcn_mfma_i32_32x32x32_i8(av, bv[j], acc[i + j], 0, 0, 0);
+                __builtin_amdgcn_sched_barrier(0);
+            }
+        } else {
+#pragma unroll
+            for (int i = 0; i < D; ++i) {
+                const v4i av = *(const v4i*)(st + i * PANEL + (wm + r) * 32 + 16 * h);
+#pragma unroll
+                for (int j = 0; j < D; ++j)
+                    acc[i + j] = __builtin_amdgcn_mfma_i32_32x32x32_i8(av, bv[j], acc[i + j], 0, 0, 0);
+            }
+        }
+        // stage s + 1 landed for this wave: newer are the DMAs of stages s + 2 and s + 3 that were issued
+        if (s + 1 < NST) {
+            const int newer = (s + 3 < NST ? s + 3 : NST - 1) - (s + 1);
+            if (newer == 2) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(2 * D) : "memory");
+            else if (newer == 1) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(D) : "memory");
+            else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+            barrier();
+        }
+    }
+    mfma_epilogue<D, FAC>(a, acc, l, mb + wm, (uint32_t)(pb + wp), r, h, Ppad);
+}
+
 size_t mod_gemm_mfma_ws(uint32_t P, int L, int D) {
     const uint64_t Ppad = ((uint64_t)P + 63) / 64 * 64;
     return (size_t)L * D * Ppad * MK + (size_t)L * 2 * Ppad * 8;   // digit planes, then the factored d0
@@ -615,8 +703,16 @@ static int launch_factored(const ModGemmArgs& a, int L, hipStream_t s) {
         int l1 = l0 + 1;
         while (l1 < L && (a.limbD ? std::max(a.limbD[l1], 5) : a.D) == d) ++l1;
         const dim3 grid(2 * Ppad / 64, FK / 64, l1 - l0);
-        if (d == 5) hipLaunchKernelGGL((mod_gemm_mfma_lds_kernel<5, true>), grid, dim3(256), 0, s, f, Ppad, l0);
-        else hipLaunchKernelGGL((mod_gemm_mfma_lds_kernel<6, true>), grid, dim3(256), 0, s, f, Ppad, l0);
+        if (a.pipe == 2) {
+            if (d == 5) hipLaunchKernelGGL((mod_gemm_mfma_ring_kernel<5, true, true>), grid, dim3(256), 0, s, f, Ppad, l0);
+            else hipLaunchKernelGGL((mod_gemm_mfma_ring_kernel<6, true, true>), grid, dim3(256), 0, s, f, Ppad, l0);
+        } else if (a.pipe == 1) {
+            if (d == 5) hipLaunchKernelGGL((mod_gemm_mfma_ring_kernel<5, true, false>), grid, dim3(256), 0, s, f, Ppad, l0);
+            else hipLaunchKernelGGL((mod_gemm_mfma_ring_kernel<6, true, false>), grid, dim3(256), 0, s, f, Ppad, l0);
+        } else {
+            if (d == 5) hipLaunchKernelGGL((mod_gemm_mfma_lds_kernel<5, true>), grid, dim3(256), 0, s, f, Ppad, l0);
+            else hipLaunchKernelGGL((mod_gemm_mfma_lds_kernel<6, true>), grid, dim3(256), 0, s, f, Ppad, l0);
+        }
         MFHE_CHECK_LAUNCH("mod_gemm_mfma_lds_kernel (factored)");
         l0 = l1;
     }
@@ -655,7 +751,11 @@ int launch_mod_gemm(const ModGemmArgs& a, int L, hipStream_t s) {
             switch (d) {
 #define MFHE_MFMA_CASE(dd)                                                                                    \
     case dd:                                                                                                  \
-        if (a.lds_stage) hipLaunchKernelGGL((mod_gemm_mfma_lds_kernel<dd, false>), grid, dim3(256), 0, s, a, Ppad, l0); \
+        if (a.lds_stage && a.pipe == 2)                                                                       \
+            hipLaunchKernelGGL((mod_gemm_mfma_ring_kernel<dd, false, (dd <= 5)>), grid, dim3(256), 0, s, a, Ppad, l0); \
+        else if (a.lds_stage && a.pipe == 1)                                                                  \
+            hipLaunchKernelGGL((mod_gemm_mfma_ring_kernel<dd, false, false>), grid, dim3(256), 0, s, a, Ppad, l0); \
+        else if (a.lds_stage) hipLaunchKernelGGL((mod_gemm_mfma_lds_kernel<dd, false>), grid, dim3(256), 0, s, a, Ppad, l0); \
         else hipLaunchKernelGGL(mod_gemm_mfma_kernel<dd>, grid, dim3(256), 0, s, a, Ppad, l0);                 \
         break;
                 MFHE_MFMA_CASE(5)

@@ -576,6 +576,7 @@ static int use_mfma(mfhe_ctx* c, ModGemmArgs& a, const uint64_t* A, int L) {
     a.limbD = (a.aL && (int)c->wDl.size() == L) ? c->wDl.data() : nullptr;
     a.epi = c->d_wepi;
     a.lds_stage = c->wcrt_mfma != 2;
+    a.pipe = c->wcrt_pipe;
     // mode 1: the forward transform of a per-limb V runs factored (half the MACs, gemm.hip)
     if (c->wcrt_mfma == 1 && A == c->d_wV && a.aL && c->d_wZdig && a.epi) {
         a.Adig = c->d_wZdig;

@@ -99,6 +99,7 @@ struct mfhe_ctx {
     int8_t* d_wZdig = nullptr;   // [L][wD][256][256] digits of Z[i][k] = zeta^((i+1)(k+1)) (factored forward W-CRT)
     double* d_wfold = nullptr;   // [L][16] factored forward fold constants (gemm.hip mfma_digitize_fold_kernel)
     int wcrt_mfma = 1;           // MFHE_OPT_WCRT_MFMA
+    int wcrt_pipe = 0;           // MFHE_OPT_WCRT_PIPE
     int cgemm_mfma = 1;          // MFHE_OPT_CGEMM_MFMA
     int he_fused = 1;            // MFHE_OPT_HE_FUSED
     int limb_base = 0;           // residue shard: global index of this context's limb 0 (mfhe_ctx_set_limb_shard)

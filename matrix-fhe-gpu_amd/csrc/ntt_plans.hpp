@@ -14,7 +14,6 @@
 #include "mfhe_ctx.hpp"
 #include "ntt_coldb.hpp"
 #include "ntt_fused.hpp"
-#include "ntt_fused_db.hpp"
 
 // Groups (contiguous rows) per block-pass workgroup.  N = 2^16: 4 rows (64 threads, 8.7 KiB LDS) rather than 16
 // (256 threads, 34.9 KiB): the block pass gains from residency and 16-row tiles are LDS-bound at 4 per CU;
@@ -321,60 +320,6 @@ static int fused(const NttJob<TS>& j, hipStream_t st) {
     return MFHE_OK;
 }
 
-// Forward N = 2^16 F64, fused with the next pass-1 tile's LDS-DMA in flight (ntt_fused_db.hpp),
-// MFHE_OPT_NTT_FUSED = 2.  Same queues / arrival counters / sync buffer as fused().
-template <class TS>
-static int fused_db(const NttJob<TS>& j, hipStream_t st) {
-    using C = FusedDb;
-    const uint64_t npl = j.batch * (uint64_t)j.nl;
-    const uint32_t K = C::K;
-    if (npl * K >= 0xFFFFFFFFull) return set_error(MFHE_EINVAL, "NTT batch too large for one fused launch");
-    mfhe_ctx* c = j.ctx;
-    if (c->xcc_nq == 0) return set_error(MFHE_ENOTREADY, "fused NTT: XCC census missing (set MFHE_OPT_NTT_FUSED)");
-    static int occ = 0;
-    if (occ == 0) {
-        int o = 0;
-        if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&o, ntt_fused_db_kernel<0>, C::NT, C::LDS_BYTES) != hipSuccess ||
-            o < 1)
-            o = 1;
-        occ = o;
-    }
-    const int per_cu = (j.wg_per_cu > 0 && j.wg_per_cu < 16) ? std::min(j.wg_per_cu, occ) : occ;
-    const uint32_t grid = (uint32_t)std::max(8, per_cu * j.num_cus);
-    const uint32_t nq = (uint32_t)c->xcc_nq;
-    const uint64_t cap = (npl + nq - 1) / nq + 1;
-    const size_t need = sizeof(FusedSync) + (size_t)kFusedXcc * cap * sizeof(uint32_t);
-    if (c->fused_bytes < need) {
-        if (c->fused_buf) MFHE_HIP(hipFree(c->fused_buf));
-        c->fused_buf = nullptr;
-        c->fused_bytes = 0;
-        MFHE_HIP(hipMalloc(&c->fused_buf, need));
-        c->fused_bytes = need;
-    }
-    MFHE_HIP(hipMemsetAsync(c->fused_buf, 0, need, st));
-    FusedArgs<TS> f{};
-    PassArgs<TS>& a = f.p;
-    a.data = j.data;
-    a.tw = j.tw;
-    a.limbs = j.limbs;
-    a.batch = j.batch;
-    a.nl = j.nl;
-    a.start_limb = j.start_limb;
-    a.logN = j.logN;
-    a.nblocks = (uint32_t)(npl * K);
-    f.sync = (FusedSync*)c->fused_buf;
-    f.arr = (uint32_t*)((char*)c->fused_buf + sizeof(FusedSync));
-    f.cap = (uint32_t)cap;
-    f.K = K;
-    f.npl = (uint32_t)npl;
-    f.lag = (uint32_t)c->ntt_fused_lag;
-    f.nq = nq;
-    for (int x = 0; x < kFusedXcc; ++x) f.qmap[x] = c->xcc_qmap[x];
-    hipLaunchKernelGGL(ntt_fused_db_kernel<0>, dim3(grid), dim3(C::NT), C::LDS_BYTES, st, f);
-    MFHE_CHECK_LAUNCH("ntt_fused_db_kernel launch");
-    return MFHE_OK;
-}
-
 template <class A, class TS, bool INV>
 static int run_phantom(const NttJob<TS>& j, hipStream_t st) {
     // auto: N = 2^14 runs two passes (7 + 7, 8-row block tiles): at C2 +1% forward, +7% inverse over the single
@@ -382,9 +327,6 @@ static int run_phantom(const NttJob<TS>& j, hipStream_t st) {
     // (profiles/r02_c2_plans2.txt)
     const bool two = j.logN > 14 || (j.plan == 2 && j.logN >= 12) || (j.plan == 0 && j.logN == 14);
     if (!two) return run_single<A, TS, INV, false>(j, st);
-    if constexpr (!INV && std::is_same<A, ArithF64>::value) {
-        if (j.ctx && j.ctx->ntt_fused == 2 && j.logN == 16 && j.limbs) return fused_db(j, st);
-    }
     if (j.ctx && j.ctx->ntt_fused && j.logN >= 15) {
         switch (j.logN) {
             case 15: return fused<A, TS, 8, 16, 7, 32, INV>(j, st);

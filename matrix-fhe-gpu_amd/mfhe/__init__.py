@@ -28,6 +28,7 @@ OPT_NTT_FUSED, OPT_NTT_FUSED_LAG, OPT_NTT_FUSED_ERRORS, OPT_WCRT_MFMA = 6, 7, 8,
 OPT_CGEMM_MFMA, OPT_HE_FUSED, OPT_TRACE_SPLIT = 10, 11, 12
 XCHG_ALLGATHER, XCHG_ALLTOALL = 0, 1
 OPT_NTT_PACK = 13
+OPT_WCRT_PIPE = 14
 COMM_ID_BYTES = 128
 
 #: reference parameters (include/core/config.h:7-52)

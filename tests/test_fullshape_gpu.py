@@ -100,8 +100,8 @@ def test_c2_full_shape(mfhe, orc, dig):
     _run_ntt_config(mfhe, orc, dig, "c2")
 
 
-@pytest.mark.parametrize("arith,fused,prefetch", [(0, 0, None), (2, 0, None), (0, 1, None), (0, 2, None), (0, 0, 0)],
-                         ids=["f64", "u64", "f64-fused", "f64-fused-dma", "f64-plain-colpass"])
+@pytest.mark.parametrize("arith,fused,prefetch", [(0, 0, None), (2, 0, None), (0, 1, None), (0, 0, 0), (2, 0, 0)],
+                         ids=["f64", "u64", "f64-fused", "f64-plain-colpass", "u64-plain-colpass"])
 def test_c3_full_shape(mfhe, orc, dig, arith, fused, prefetch):
     _run_ntt_config(mfhe, orc, dig, "c3", arith, fused, prefetch)
 
@@ -153,7 +153,7 @@ def test_c3_encode_ntt_intt_decode_full_shape(mfhe, orc, dig):
     torch.cuda.empty_cache()
 
 
-@pytest.mark.parametrize("fused,lag", [(1, 8), (1, 12), (2, 8), (2, 12)])
+@pytest.mark.parametrize("fused,lag", [(1, 8), (1, 12)])
 def test_c3_full_shape_fused_long_lag(mfhe, orc, dig, fused, lag):
     """The fused plans at the C3 shape with a long pass-2 lag (more polynomials' intermediates in flight per XCD
     than its L2 holds)."""

@@ -471,7 +471,9 @@ def test_kat7_kat8_encrypt_decrypt_reference_geometry(mfhe, pattern, tol):
 def test_wcrt_mfma_matches_valu_and_oracle(mfhe, orc, n, L):
     """W-CRT GEMM on i8 MFMA (digit-split exact product, gemm.hip) == the u128 VALU kernel == oracle,
     all three layouts (matrix->poly, poly->matrix, vector), bit-exact.  Modes: 1 = LDS-staged with the
-    forward factored through 771 = 3 x 257 (default), 3 = LDS-staged dense, 2 = global fragments, 0 = VALU."""
+    forward factored through 771 = 3 x 257 (default), 3 = LDS-staged dense, 2 = global fragments, 0 = VALU; the
+    LDS-staged modes under each K pipeline (MFHE_OPT_WCRT_PIPE 0: two 64-k stages, 1: 4-slot 32-k ring, 2: ring
+    with one-ahead A-fragment reads)."""
     import torch
     log_n = n.bit_length() - 1
     ctx = mfhe.Context(RNS[:L], log_n, CONV)
@@ -479,8 +481,10 @@ def test_wcrt_mfma_matches_valu_and_oracle(mfhe, orc, n, L):
     rng = np.random.default_rng(n * 100 + L)
     x = _rand_mat(rng, n, L)
     outs = {}
-    for mf in (1, 3, 2, 0):
+    modes = [(1, 0), (1, 1), (1, 2), (3, 0), (3, 1), (3, 2), (2, 0), (0, 0)]
+    for mf, pipe in modes:
         ctx.set_option(mfhe.OPT_WCRT_MFMA, mf)
+        ctx.set_option(mfhe.OPT_WCRT_PIPE, pipe)
         d = _dev(mfhe, x)
         f = torch.empty_like(d)
         ctx.wcrt_fwd(d, f)
@@ -490,18 +494,18 @@ def test_wcrt_mfma_matches_valu_and_oracle(mfhe, orc, n, L):
         vo = torch.empty(v.size, dtype=torch.int64, device="cuda")
         ctx.wcrt_fwd_vector(_dev(mfhe, v), vo)
         torch.cuda.synchronize()
-        outs[mf] = (mfhe.to_host_u64(f), mfhe.to_host_u64(b), mfhe.to_host_u64(vo))
-        np.testing.assert_array_equal(outs[mf][1], x)
+        outs[mf, pipe] = (mfhe.to_host_u64(f), mfhe.to_host_u64(b), mfhe.to_host_u64(vo))
+        np.testing.assert_array_equal(outs[mf, pipe][1], x)
         rng = np.random.default_rng(n * 100 + L)   # same vector input for both runs
         _rand_mat(rng, n, L)
-    for mf in (1, 3, 2):
-        for a, b in zip(outs[mf], outs[0]):
+    for key in modes[:-1]:
+        for a, b in zip(outs[key], outs[0, 0]):
             np.testing.assert_array_equal(a, b)
     if n <= 8:
         h = orc.HE(n, RNS[:L], 2.0 ** 35)
         ref = np.zeros_like(x)
         orc.L.orc_wntt_forward_matrix(P(x), P(ref), n, L, 512, P(U64(RNS[:L])), orc.L.orc_he_V(h.h))
-        np.testing.assert_array_equal(outs[1][0], ref)
+        np.testing.assert_array_equal(outs[1, 0][0], ref)
 
 
 @pytest.mark.parametrize("n,log_n,L", [(8, 3, 11), (64, 6, 11), (16, 4, 3)])

@@ -78,12 +78,3 @@ def test_column_pass_dma_waits_match_the_instruction_mix(inv, arith):
     assert not any("vmcnt" in l for l in lines[b0 + 1:s0]), [l for l in lines[b0 + 1:s0] if "vmcnt" in l]
     # the stores' base is uniform: no readfirstlane (waterfall) loop around them
     assert "s_cbranch_execnz" not in "\n".join(lines[s0:s0 + 80]), "stores wrapped in a waterfall loop"
-
-
-def test_fused_dma_kernel_has_no_spills_and_one_prefetch_wait():
-    """ntt_fused_db_kernel (MFHE_OPT_NTT_FUSED = 2): no scratch, and the only non-zero vmcnt wait is the vmcnt(8)
-    that leaves the next tile's 8 DMA instructions in flight."""
-    asm = _kernel_asm(r"_ZN4mfhe19ntt_fused_db_kernel[^>]*")
-    assert "scratch_" not in asm
-    waits = {int(v) for v in re.findall(r"s_waitcnt[^\n]*vmcnt\((\d+)\)", asm)}
-    assert waits == {0, 8}, waits

@@ -307,30 +307,6 @@ def test_fused_two_pass_matches_oracle(mfhe, orc, log_n, batch, nl, lag):
         assert ctx.get_option(mfhe.OPT_NTT_FUSED_ERRORS) == 0
 
 
-@pytest.mark.parametrize("batch,nl,lag", [(1, 1, 2), (5, 3, 1), (40, 3, 4), (9, 4, 7), (64, 2, 3)])
-def test_fused_dma_matches_oracle(mfhe, orc, batch, nl, lag):
-    """MFHE_OPT_NTT_FUSED = 2 (N = 2^16 forward, FP64): the fused launch with the next pass-1 tile's LDS-DMA in
-    flight (ntt_fused_db.hpp) -- bit-exact vs the oracle on a limb sub-range, limb changes inside a queue (the
-    twiddle table reload), every lag, and no spin timeout or unmapped XCC; the inverse of mode 2 is the r02
-    fused kernel and must round-trip."""
-    import torch
-    N = 1 << 16
-    moduli = orc.gen_primes(50, 4 * N, nl + 1)
-    ctx = mfhe.Context(moduli, 16)
-    ctx.set_option(mfhe.OPT_NTT_FUSED, 2)
-    ctx.set_option(mfhe.OPT_NTT_FUSED_LAG, lag)
-    data = rand_residues(np.random.default_rng(11 * batch + lag), batch, moduli[1:], N)
-    d = mfhe.to_device_u64(data)
-    ctx.ntt_fwd(d, batch=batch, start_limb=1, nlimbs=nl)
-    torch.cuda.synchronize()
-    np.testing.assert_array_equal(mfhe.to_host_u64(d), orc.phantom_fwd(data, nl, 16, moduli[1:]))
-    assert ctx.get_option(mfhe.OPT_NTT_FUSED_ERRORS) == 0
-    ctx.ntt_inv(d, batch=batch, start_limb=1, nlimbs=nl)
-    torch.cuda.synchronize()
-    np.testing.assert_array_equal(mfhe.to_host_u64(d), data)
-    assert ctx.get_option(mfhe.OPT_NTT_FUSED_ERRORS) == 0
-
-
 @pytest.mark.gpu
 @pytest.mark.parametrize("batch,nl", [(3, 2), (17, 1)])
 def test_packed_intermediate_matches_oracle(mfhe, orc, batch, nl):

@@ -25,6 +25,8 @@ def main():
     import os
     if os.environ.get("MFHE_WCRT_MODE"):
         ctx.set_option(9, int(os.environ["MFHE_WCRT_MODE"]))   # MFHE_OPT_WCRT_MFMA
+    if os.environ.get("MFHE_WCRT_PIPE"):
+        ctx.set_option(14, int(os.environ["MFHE_WCRT_PIPE"]))  # MFHE_OPT_WCRT_PIPE
     if os.environ.get("MFHE_CGEMM_MODE"):
         ctx.set_option(10, int(os.environ["MFHE_CGEMM_MODE"]))  # MFHE_OPT_CGEMM_MFMA
     t_ctx = time.perf_counter() - t0
