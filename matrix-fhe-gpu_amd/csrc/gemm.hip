@@ -289,11 +289,21 @@ __device__ __forceinline__ uint64_t balanced_bytes(double v) {   // v integral, 
     constexpr uint64_t kOff = 0x8080808080808080ull >> (64 - 8 * D);
     return (uint64_t)__double_as_longlong(v + kMagic) - ((uint64_t)__double_as_longlong(kMagic) - kOff);
 }
+// digit planes the GEMM reads per limb (max(limbD, 5), <= D): planes past it are never read, so never written
+struct PlaneCounts {
+    uint8_t n[64];   // limbs >= 64: all D
+};
+static PlaneCounts plane_counts(const ModGemmArgs& a, int L) {
+    PlaneCounts pc;
+    for (int l = 0; l < 64; ++l) pc.n[l] = (uint8_t)(a.limbD && l < L ? std::max(a.limbD[l], 5) : a.D);
+    return pc;
+}
+
 // one thread: column p (of Ppad; zero past P), one 32-k panel; B (k, p) via the (sbK, sbY, log_n) map
 template <int D>
 __global__ __launch_bounds__(256) void mfma_digitize_kernel(const uint64_t* __restrict__ B, uint64_t bL,
                                                             uint64_t sbK, uint64_t sbY, int log_n, uint32_t P,
-                                                            uint32_t Ppad, int8_t* __restrict__ out) {
+                                                            uint32_t Ppad, int8_t* __restrict__ out, PlaneCounts pc) {
     const uint32_t p = blockIdx.x * 256 + threadIdx.x;
     const int kc = blockIdx.y;
     const int l = blockIdx.z;
@@ -315,8 +325,10 @@ __global__ __launch_bounds__(256) void mfma_digitize_kernel(const uint64_t* __re
             pk[i][kk >> 2] |= v << (8 * (kk & 3));
         }
     }
+    const int nd = l < 64 ? pc.n[l] : D;
 #pragma unroll
     for (int i = 0; i < D; ++i) {
+        if (i >= nd) break;
         int8_t* o = out + (((uint64_t)l * D + i) * (MK / 32) + kc) * Ppad * 32 + (uint64_t)p * 32;
         *(v4i*)o = v4i{(int)pk[i][0], (int)pk[i][1], (int)pk[i][2], (int)pk[i][3]};
         *(v4i*)(o + 16) = v4i{(int)pk[i][4], (int)pk[i][5], (int)pk[i][6], (int)pk[i][7]};
@@ -345,7 +357,8 @@ template <int D>
 __global__ __launch_bounds__(256) void mfma_digitize_fold_kernel(const uint64_t* __restrict__ B, uint64_t bL,
                                                                  uint64_t sbK, uint64_t sbY, int log_n, uint32_t P,
                                                                  uint32_t Ppad, const double* __restrict__ fold,
-                                                                 int8_t* __restrict__ out, uint64_t* __restrict__ d0) {
+                                                                 int8_t* __restrict__ out, uint64_t* __restrict__ d0,
+                                                                 PlaneCounts pc) {
     const uint32_t p = blockIdx.x * 128 + (threadIdx.x >> 1);
     const int hf = threadIdx.x & 1;
     const int kc = blockIdx.y;   // panel: r2 = 32 kc + 16 hf + 1 .. 32 kc + 16 hf + 16
@@ -402,10 +415,12 @@ __global__ __launch_bounds__(256) void mfma_digitize_fold_kernel(const uint64_t*
         for (int ap = 0; ap < 2; ++ap)
             d0[((uint64_t)l * 2 + ap) * Ppad + p] = ar.canon(ar.mulmod(x1, c1[ap][0]) + ar.mulmod(x2, c2[ap][0]));
     }
+    const int nd = l < 64 ? pc.n[l] : D;
 #pragma unroll
     for (int ap = 0; ap < 2; ++ap)
 #pragma unroll
         for (int i = 0; i < D; ++i) {
+            if (i >= nd) break;
             int8_t* o = out + ((((uint64_t)l * D + i) * (FK / 32) + kc) * 2 * Ppad + (uint64_t)ap * Ppad + p) * 32 + hf * 16;
             const uint32_t* w = pk[ap][i];
             *(v4i*)o = v4i{(int)(w[0] ^ 0x80808080u), (int)(w[1] ^ 0x80808080u), (int)(w[2] ^ 0x80808080u),
@@ -583,13 +598,14 @@ __global__ __launch_bounds__(256, D <= 5 ? 2 : 1) void mod_gemm_mfma_lds_kernel(
     mfma_epilogue<D, FAC>(a, acc, l, mb + wm, (uint32_t)(pb + wp), r, h, Ppad);
 }
 
-// Ring variant (MFHE_OPT_WCRT_PIPE >= 1): the same tile, digit planes and epilogue, but the K loop runs over
-// 32-k stages (one panel per digit plane per operand, 4 D KiB) held in a 4-slot LDS ring (80 KiB at D = 5: still
-// 2 workgroups per CU).  Stage s + 3 is DMA'd while stage s is multiplied, so a stage's bytes have three stage
-// times to land instead of one, and the wait at the end of stage s is a counted vmcnt that leaves stages s + 2
-// and s + 3 in flight (D DMA instructions per thread per stage; nothing else in the loop touches vector memory).
-// The barrier after it is a raw s_barrier (__syncthreads' fence would wait for the DMAs in flight).  Slot
-// (s + 3) & 3 = (s - 1) & 3 was last read in stage s - 1, which every wave has left at that barrier.
+// Ring variant (MFHE_OPT_WCRT_PIPE 2 / 3, and 0 = auto on the factored launch): the same tile, digit planes and
+// epilogue, but the K loop runs over 32-k stages (one panel per digit plane per operand, 4 D KiB) held in a
+// 4-slot LDS ring (80 KiB at D = 5: still 2 workgroups per CU).  Stage s + 3 is DMA'd while stage s is
+// multiplied, so a stage's bytes have three stage times to land instead of one, and the wait at the end of
+// stage s is a counted vmcnt that leaves stages s + 2 and s + 3 in flight (D DMA instructions per thread per
+// stage; nothing else in the loop touches vector memory).  The barrier after it is a raw s_barrier
+// (__syncthreads' fence would wait for the DMAs in flight).  Slot (s + 3) & 3 = (s - 1) & 3 was last read in
+// stage s - 1, which every wave has left at that barrier.
 // AHEAD: the next A fragment's LDS read is issued before the current fragment's D MFMAs (sched_barrier-pinned),
 // so its latency hides behind them instead of being waited for in front of them (D <= 5 only: at D >= 6 the
 // extra fragment spills).
@@ -693,20 +709,21 @@ static int launch_factored(const ModGemmArgs& a, int L, hipStream_t s) {
     ModGemmArgs f = a;
     f.d0 = (uint64_t*)(a.Bdig + (size_t)L * a.D * Ppad * MK);
     const dim3 gd((Ppad + 127) / 128, FK / 32, L);
+    const PlaneCounts pc = plane_counts(a, L);
     if (a.D == 5) hipLaunchKernelGGL(mfma_digitize_fold_kernel<5>, gd, dim3(256), 0, s, a.B, a.bL, a.sbK, a.sbY, a.log_n,
-                                     a.P, Ppad, a.fold, a.Bdig, f.d0);
+                                     a.P, Ppad, a.fold, a.Bdig, f.d0, pc);
     else hipLaunchKernelGGL(mfma_digitize_fold_kernel<6>, gd, dim3(256), 0, s, a.B, a.bL, a.sbK, a.sbY, a.log_n, a.P,
-                            Ppad, a.fold, a.Bdig, f.d0);
+                            Ppad, a.fold, a.Bdig, f.d0, pc);
     MFHE_CHECK_LAUNCH("mfma_digitize_fold_kernel");
     for (int l0 = 0; l0 < L;) {
         const int d = a.limbD ? std::max(a.limbD[l0], 5) : a.D;
         int l1 = l0 + 1;
         while (l1 < L && (a.limbD ? std::max(a.limbD[l1], 5) : a.D) == d) ++l1;
         const dim3 grid(2 * Ppad / 64, FK / 64, l1 - l0);
-        if (a.pipe == 2) {
+        if (a.pipe == 3) {
             if (d == 5) hipLaunchKernelGGL((mod_gemm_mfma_ring_kernel<5, true, true>), grid, dim3(256), 0, s, f, Ppad, l0);
             else hipLaunchKernelGGL((mod_gemm_mfma_ring_kernel<6, true, true>), grid, dim3(256), 0, s, f, Ppad, l0);
-        } else if (a.pipe == 1) {
+        } else if (a.pipe != 1) {   // 0 (auto) and 2: the ring (K = 256: four 64-k stages leave the fill exposed)
             if (d == 5) hipLaunchKernelGGL((mod_gemm_mfma_ring_kernel<5, true, false>), grid, dim3(256), 0, s, f, Ppad, l0);
             else hipLaunchKernelGGL((mod_gemm_mfma_ring_kernel<6, true, false>), grid, dim3(256), 0, s, f, Ppad, l0);
         } else {
@@ -732,7 +749,7 @@ int launch_mod_gemm(const ModGemmArgs& a, int L, hipStream_t s) {
 #define MFHE_DIG_CASE(d)                                                                                         \
     case d:                                                                                                      \
         hipLaunchKernelGGL(mfma_digitize_kernel<d>, gd, dim3(256), 0, s, a.B, a.bL, a.sbK, a.sbY, a.log_n, a.P,   \
-                           Ppad, a.Bdig);                                                                        \
+                           Ppad, a.Bdig, plane_counts(a, L));                                                    \
         break;
             MFHE_DIG_CASE(5)
             MFHE_DIG_CASE(6)
@@ -751,9 +768,9 @@ int launch_mod_gemm(const ModGemmArgs& a, int L, hipStream_t s) {
             switch (d) {
 #define MFHE_MFMA_CASE(dd)                                                                                    \
     case dd:                                                                                                  \
-        if (a.lds_stage && a.pipe == 2)                                                                       \
+        if (a.lds_stage && a.pipe == 3)                                                                       \
             hipLaunchKernelGGL((mod_gemm_mfma_ring_kernel<dd, false, (dd <= 5)>), grid, dim3(256), 0, s, a, Ppad, l0); \
-        else if (a.lds_stage && a.pipe == 1)                                                                  \
+        else if (a.lds_stage && a.pipe == 2)                                                                  \
             hipLaunchKernelGGL((mod_gemm_mfma_ring_kernel<dd, false, false>), grid, dim3(256), 0, s, a, Ppad, l0); \
         else if (a.lds_stage) hipLaunchKernelGGL((mod_gemm_mfma_lds_kernel<dd, false>), grid, dim3(256), 0, s, a, Ppad, l0); \
         else hipLaunchKernelGGL(mod_gemm_mfma_kernel<dd>, grid, dim3(256), 0, s, a, Ppad, l0);                 \

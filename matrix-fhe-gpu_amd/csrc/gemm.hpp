@@ -37,8 +37,8 @@ struct ModGemmArgs {
     const int* limbD = nullptr;  // host: digits limb l needs (<= D); null = D for every limb
     const double* epi = nullptr; // [L][8] FP64 epilogue (q, 1/q, centred 2^32k mod q); null = integer epilogue
     bool lds_stage = true;       // LDS-staged MFMA kernel (false: fragments straight from global memory)
-    int pipe = 0;                // LDS-staged K pipeline (MFHE_OPT_WCRT_PIPE): 0 two 64-k stages, 1 4-slot 32-k ring,
-                                 // 2 ring + one-ahead A-fragment reads
+    int pipe = 0;                // LDS-staged K pipeline (MFHE_OPT_WCRT_PIPE): 0 auto (factored: ring, dense: two
+                                 // 64-k stages), 1 two 64-k stages, 2 4-slot 32-k ring, 3 ring + one-ahead A reads
     // factored forward W-CRT (gemm.hip, 771 = 3 x 257): Adig holds the [L][D][256][256] planes of
     // Z[i][k] = zeta^((i+1)(k+1)) and fold [L][16] its FP64 fold constants; null = dense GEMM
     const double* fold = nullptr;
