@@ -101,20 +101,40 @@ struct ArithF64 {
 struct ArithU64 {
     using T = uint64_t;
     using Tw = ulonglong2;   // (w, floor(w 2^64 / q))
-    uint64_t q, two_q;
+    // q < 2^62.  Every 64-bit subtraction of a value is an addition of its negation (one v_lshl_add_u64, no
+    // carry through VCC: a v_sub_co / v_subb_co pair reads the VCC the first one wrote, which costs wait
+    // states on gfx950), and every conditional subtraction is a select on the sign of the difference
+    // (v_bfi_b32 on a v_ashrrev mask, no compare).
+    uint64_t q, two_q, nq, n2q;   // nq = -q, n2q = -2q (mod 2^64)
 
-    __device__ __forceinline__ explicit ArithU64(const LimbConst& c) : q(c.q), two_q(2 * c.q) {}
+    __device__ __forceinline__ explicit ArithU64(const LimbConst& c)
+        : q(c.q), two_q(2 * c.q), nq(0 - c.q), n2q(0 - 2 * c.q) {
+        // held as values: otherwise x + n2q is re-derived from q as a v_mad_u64_u32 by -2 (a quarter-rate
+        // multiply) in every butterfly
+        asm volatile("" : "+v"(nq));
+        asm volatile("" : "+v"(n2q));
+    }
 
     __device__ __forceinline__ static uint64_t from_u64(uint64_t x) { return x; }
     __device__ __forceinline__ static uint64_t from_raw(uint64_t x) { return x; }
     __device__ __forceinline__ static uint64_t to_raw(uint64_t x) { return x; }
 
-    // Shoup: v*w - hi64(v*w')*q in [0, 2q) for any v < 2^64
+    // d = x - m (mod 2^64) with 0 <= x < 2m, m <= 2^63: x if d wrapped (top bit set), else d -- one shift for
+    // the mask and a bit-field insert per half
+    __device__ __forceinline__ static uint64_t sel_sub(uint64_t x, uint64_t d) {
+        const uint32_t dl = (uint32_t)d, dh = (uint32_t)(d >> 32), xl = (uint32_t)x, xh = (uint32_t)(x >> 32);
+        const uint32_t msk = (uint32_t)((int32_t)dh >> 31);
+        uint32_t rl, rh;
+        asm("v_bfi_b32 %0, %1, %2, %3" : "=v"(rl) : "v"(msk), "v"(xl), "v"(dl));
+        asm("v_bfi_b32 %0, %1, %2, %3" : "=v"(rh) : "v"(msk), "v"(xh), "v"(dh));
+        return ((uint64_t)rh << 32) | rl;
+    }
+    // Shoup: v*w + hi64(v*w')*(-q) in [0,2q) for any v < 2^64
     __device__ __forceinline__ uint64_t mulmod(uint64_t v, Tw w) const {
-        return v * w.x - __umul64hi(v, w.y) * q;
+        return v * w.x + __umul64hi(v, w.y) * nq;
     }
     __device__ __forceinline__ uint64_t reduce(uint64_t x) const {   // [0,4q) -> [0,2q)
-        return (x >= two_q) ? x - two_q : x;
+        return sel_sub(x, x + n2q);
     }
     // Harvey CT: u in [0,4q), v < 2^64 -> outputs in [0,4q)
     __device__ __forceinline__ void ct(uint64_t& u, uint64_t& v, Tw w) const {
@@ -132,8 +152,8 @@ struct ArithU64 {
     __device__ __forceinline__ void gs_lazy(uint64_t& u, uint64_t& v, Tw w) const { gs(u, v, w); }
     __device__ __forceinline__ uint64_t round_reduce(uint64_t x) const { return x; }
     __device__ __forceinline__ uint64_t canon(uint64_t x) const {
-        x = (x >= two_q) ? x - two_q : x;
-        return (x >= q) ? x - q : x;
+        x = sel_sub(x, x + n2q);
+        return sel_sub(x, x + nq);
     }
 };
 
