@@ -560,7 +560,7 @@ extern "C" int mfhe_ctx_set_option(mfhe_ctx* c, int opt, int64_t v) {
             c->ntt_wg_per_cu = (int)v;
             return MFHE_OK;
         case MFHE_OPT_NTT_PREFETCH:
-            if (v < 0 || v > 3) return set_error(MFHE_EINVAL, "prefetch must be 0, 1, 2 or 3");
+            if (v < 0 || v > 2) return set_error(MFHE_EINVAL, "prefetch must be 0, 1 or 2");
             c->ntt_prefetch = (int)v;
             return MFHE_OK;
         case MFHE_OPT_NTT_PACK:

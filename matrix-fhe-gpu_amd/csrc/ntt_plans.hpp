@@ -13,7 +13,6 @@
 
 #include "mfhe_ctx.hpp"
 #include "ntt_coldb.hpp"
-#include "ntt_blkdb.hpp"
 #include "ntt_fused.hpp"
 
 // Groups (contiguous rows) per block-pass workgroup.  N = 2^16: 4 rows (64 threads, 8.7 KiB LDS) rather than 16
@@ -162,53 +161,6 @@ static int launch_col_db(const NttJob<TS>& j, hipStream_t st) {
     return MFHE_OK;
 }
 
-// block pass with the next tile's DMA in flight (ntt_blkdb.hpp), MFHE_OPT_NTT_PREFETCH = 3: N = 2^16 FP64, the
-// forward's second pass or (INV) the inverse's first
-template <bool INV>
-static bool blk_db_usable() {
-    static int ok = -1;
-    if (ok < 0) {
-        hipFuncAttributes fa{};
-        ok = hipFuncGetAttributes(&fa, reinterpret_cast<const void*>(ntt_blk_db_kernel<INV>)) == hipSuccess &&
-             fa.localSizeBytes == 0;
-    }
-    return ok == 1;
-}
-
-template <bool INV>
-static int launch_blk_db(const NttJob<TwSrcF>& j, hipStream_t st) {
-    using C = BlkDb;
-    const uint64_t npl = j.batch * (uint64_t)j.nl;
-    const uint64_t nb = npl << (j.logN - C::LOG_G - 4);   // 16-row tiles: 2^(logN - 8) rows per polynomial
-    if (nb == 0) return MFHE_OK;
-    if (nb > 0xFFFFFFFFull || npl >= 0xFFFFFFFFull)
-        return set_error(MFHE_EINVAL, "NTT batch too large for one launch (batch * nlimbs must be < 2^32)");
-    PassArgs<TwSrcF> a{};
-    a.data = j.data;
-    a.tw = j.tw;
-    a.limbs = j.limbs;
-    a.batch = j.batch;
-    a.nl = j.nl;
-    a.start_limb = j.start_limb;
-    a.logN = j.logN;
-    a.s0 = j.logN - C::LOG_G;
-    a.nblocks = (uint32_t)nb;
-    static int occ = 0;
-    if (occ == 0) {
-        int o = 0;
-        if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&o, ntt_blk_db_kernel<INV>, C::NT, C::LDS_BYTES) != hipSuccess ||
-            o < 1)
-            o = 1;
-        occ = o;
-    }
-    const int per_cu = j.wg_per_cu > 0 ? std::min(j.wg_per_cu, occ) : occ;
-    const uint64_t cap = std::max<uint64_t>(8, ((uint64_t)per_cu * j.num_cus) & ~7ull);
-    const uint32_t grid = (uint32_t)std::min<uint64_t>(nb, cap);
-    hipLaunchKernelGGL(ntt_blk_db_kernel<INV>, dim3(grid), dim3(C::NT), C::LDS_BYTES, st, a);
-    MFHE_CHECK_LAUNCH("ntt_blk_db_kernel launch");
-    return MFHE_OK;
-}
-
 template <int LOGN>
 struct SinglePlan {
     // 16 elements per thread (N = 2^14: 1024 threads, 128 VGPRs, 16 waves per CU).  The earlier 32 per
@@ -263,11 +215,6 @@ static int two_pass_chunk(const NttJob<TS>& c, int pass, hipStream_t st) {
         // the column pass with the next tile's DMA in flight: the forward's first pass, the inverse's second
         if (pass == (INV ? 1 : 0) && c.prefetch >= 2 && c.limbs && col_db_usable<A, TS, INV>())
             return launch_col_db<A, TS, INV>(c, st);
-    }
-    if constexpr (std::is_same<A, ArithF64>::value && std::is_same<TS, TwSrcF>::value && LOG_GA == 8 && LOG_GB == 8) {
-        // the block pass likewise (N = 2^16): the forward's second pass, the inverse's first
-        if (pass == (INV ? 0 : 1) && c.prefetch == 3 && c.limbs && blk_db_usable<INV>())
-            return launch_blk_db<INV>(c, st);
     }
     if (!INV) {
         if (pass == 0) return launch_pass<A, TS, LOG_GA, 4, NGA, true, false, false, true, false, false, true>(c, 0, st);

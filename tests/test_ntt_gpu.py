@@ -330,40 +330,6 @@ def test_packed_intermediate_matches_oracle(mfhe, orc, batch, nl):
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("arith", [1, 2], ids=["f64", "u64"])
-@pytest.mark.parametrize("batch,nl", [(1, 1), (7, 3), (33, 2)])
-def test_block_pass_dma_prefetch_matches_oracle(mfhe, orc, batch, nl, arith):
-    """MFHE_OPT_NTT_PREFETCH = 3 (ntt_blkdb.hpp: the N = 2^16 FP64 block pass -- forward second, inverse first --
-    with the next 16-row tile's LDS-DMA in flight, beside the DMA column pass): forward bit-exact vs the oracle
-    and the inverse of random input vs the oracle, on a limb sub-range, with and without chunking; the U64
-    path ignores the block-pass option and must stay exact."""
-    import torch
-    log_n = 16
-    N = 1 << log_n
-    moduli = orc.gen_primes(50, 4 * N, nl + 1)
-    ctx = mfhe.Context(moduli, log_n)
-    ctx.set_arith(arith)
-    ctx.set_option(mfhe.OPT_NTT_PREFETCH, 3)
-    assert ctx.get_option(mfhe.OPT_NTT_PREFETCH) == 3
-    data = rand_residues(np.random.default_rng(13 * batch + nl), batch, moduli[1:], N)
-    want = orc.phantom_fwd(data, nl, log_n, moduli[1:])
-    want_inv = orc.phantom_inv(data, nl, log_n, moduli[1:])
-    for chunk in (0, 2 * nl * N * 8):
-        ctx.set_option(mfhe.OPT_NTT_CHUNK_BYTES, chunk)
-        d = mfhe.to_device_u64(data)
-        ctx.ntt_fwd(d, batch=batch, start_limb=1, nlimbs=nl)
-        torch.cuda.synchronize()
-        np.testing.assert_array_equal(mfhe.to_host_u64(d), want)
-        ctx.ntt_inv(d, batch=batch, start_limb=1, nlimbs=nl)
-        torch.cuda.synchronize()
-        np.testing.assert_array_equal(mfhe.to_host_u64(d), data)
-        d = mfhe.to_device_u64(data)
-        ctx.ntt_inv(d, batch=batch, start_limb=1, nlimbs=nl)
-        torch.cuda.synchronize()
-        np.testing.assert_array_equal(mfhe.to_host_u64(d), want_inv)
-
-
-@pytest.mark.gpu
 @pytest.mark.parametrize("log_n", [15, 16, 17])
 @pytest.mark.parametrize("batch,nl", [(1, 1), (7, 3), (33, 2)])
 def test_column_pass_dma_prefetch_matches_oracle(mfhe, orc, log_n, batch, nl):
