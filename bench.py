@@ -340,7 +340,9 @@ def c4_line(world, rank, comm, barrier, reps=5):
     c_all.close()
     return {"workload": f"C4: encode->encrypt_pair->decrypt_and_decode, n=64 x 512 W-lanes, L=16 x 35-bit moduli, "
                         f"limbs sharded over {G} GPU(s) ({lg} per GPU), RCCL recombine in decode",
-            "scaling": "strong (one batch for all ranks)", **out}
+            "scaling": "strong (one batch for all ranks)",
+            "exchange": ("1-rank communicator: the sharded code path with no data exchanged" if G == 1 else
+                         f"RCCL across {G} ranks"), **out}
 
 
 def c5_line(world, rank, barrier, timed, backend, reps=2, recv_gib=2.0):

@@ -103,15 +103,23 @@ __global__ __launch_bounds__(P1::NT) void ntt_fused_kernel(FusedArgs<TS> f) {
         if (t == 0) __hip_atomic_fetch_add(&f.arr[(size_t)q * f.cap + p], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     };
     q = f.qmap[xcc_id()];
-    if (q >= Q) q = 0;
+    // an XCC the census did not see: its L2 is no queue's, so it can neither produce nor consume a hand-off.
+    // It sets err bit 4 and takes no task (it still counts its exit, and may drain as the last one out).
+    bool skip = false;
+    if (q >= Q) {
+        if (t == 0) atomicOr(&sy->err, 4u);
+        skip = true;
+        q = 0;
+    }
     bool drain = false;   // last workgroup out: draining queues nobody ran
     while (true) {
         // local polys of queue q and its task count
         const uint32_t nloc = q < f.npl ? (f.npl - q + Q - 1) / Q : 0;
         const uint32_t total = (nloc + D) * 2 * K;
-        if (t == 0) bc[0] = __hip_atomic_fetch_add(&sy->head[q][0], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        if (t == 0 && !skip) bc[0] = __hip_atomic_fetch_add(&sy->head[q][0], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         __syncthreads();
-        uint32_t task = __builtin_amdgcn_readfirstlane(bc[0]);
+        uint32_t task = skip ? total : __builtin_amdgcn_readfirstlane(bc[0]);
+        skip = false;
         while (task < total) {
             // prefetch the next task number; lane 0 publishes it at the end of this task
             uint32_t nxt = 0;
