@@ -44,7 +44,8 @@ def main():
     tot = {"fwd": [0.0, 0.0], "inv": [0.0, 0.0]}
     for k in fetch:
         if "ntt_col_db_kernel" in k:
-            inv = False                     # the DMA-prefetch column pass is forward only
+            targs = [a.strip() for a in k.split("<", 1)[1].split(">(")[0].split(",")]
+            inv = len(targs) >= 3 and targs[2] == "true"   # <A, TS, INV>: the inverse's last pass
         elif "ntt_pass_kernel" in k:
             inv = k.split("<")[1].split(",")[6].strip() == "true"   # template arg INV
         else:
