@@ -586,7 +586,7 @@ extern "C" int mfhe_ctx_set_option(mfhe_ctx* c, int opt, int64_t v) {
             c->wcrt_mfma = (int)v;
             return MFHE_OK;
         case MFHE_OPT_WCRT_PIPE:
-            if (v < 0 || v > 4) return set_error(MFHE_EINVAL, "wcrt pipe must be 0..4");
+            if (v < 0 || v > 3) return set_error(MFHE_EINVAL, "wcrt pipe must be 0, 1, 2 or 3");
             c->wcrt_pipe = (int)v;
             return MFHE_OK;
         case MFHE_OPT_CGEMM_MFMA:

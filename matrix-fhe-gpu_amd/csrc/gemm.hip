@@ -691,134 +691,6 @@ __global__ __launch_bounds__(256, D <= 5 ? 2 : 1) void mod_gemm_mfma_ring_kernel
     mfma_epilogue<D, FAC>(a, acc, l, mb + wm, (uint32_t)(pb + wp), r, h, Ppad);
 }
 
-// Persistent ring (MFHE_OPT_WCRT_PIPE 4): the ring kernel above, but each workgroup walks tiles
-// T = blockIdx.x, + gridDim.x, ... of the launch's (limb, row-tile, column-tile) space (column tile fastest, the
-// order the one-tile-per-workgroup grid dispatches), and the ring runs on across tiles: the first three stages
-// of the next tile are DMA'd while the current tile finishes, so its epilogue and the next tile's fill overlap
-// instead of each workgroup paying both once.  Stage counter g runs over (tile, stage) pairs; the wait at the
-// end of stage g leaves exactly the DMA stages issued after g + 1 in flight (epilogue stores interleaved with
-// them only make that wait stricter, never looser).
-template <int D, bool FAC>
-__global__ __launch_bounds__(256, D <= 5 ? 2 : 1) void mod_gemm_mfma_pring_kernel(ModGemmArgs a, uint32_t Ppad, int limb0,
-                                                                                  uint32_t gx, uint32_t gy, uint32_t ntiles) {
-    constexpr int KK = FAC ? FK : MK, AM = FAC ? FK : 512;
-    const uint32_t Pcols = FAC ? 2 * Ppad : Ppad;
-    constexpr int NS = 2 * D - 1;
-    constexpr int NST = KK / 32;
-    constexpr int PANEL = 64 * 32;
-    constexpr int STAGE = 2 * D * PANEL;
-    constexpr int NSLOT = 4;
-    __shared__ __attribute__((aligned(16))) int8_t lds[NSLOT * STAGE];
-    const int t = threadIdx.x, lane = t & 63, w = t >> 6;
-    const int r = lane & 31, h = lane >> 5;
-    const int wm = (w & 1) * 32, wp = (w >> 1) * 32;
-    const bool ldA = t < 128;
-    const int li = t & 127;
-    const uint64_t rows = ldA ? AM : Pcols;
-    const uint64_t pstride = rows * KK, kstride = rows * 32;
-    const int wbase = (ldA ? 0 : D * PANEL) + (li & ~63) * 16;
-    const uint32_t T0 = blockIdx.x;
-    if (T0 >= ntiles) return;
-    const uint32_t my_tiles = (ntiles - 1 - T0) / gridDim.x + 1;
-    const uint32_t G = my_tiles * NST;   // stages this workgroup runs
-    struct Tile {
-        int l, mb, pb;
-    };
-    auto tile_of = [&](uint32_t i) {   // this workgroup's i-th tile
-        const uint32_t T = T0 + i * gridDim.x;
-        Tile tl;
-        tl.pb = (int)(T % gx) * 64;
-        tl.mb = (int)((T / gx) % gy) * 64;
-        tl.l = limb0 + (int)(T / (gx * gy));
-        return tl;
-    };
-    auto issue = [&](uint32_t g) {
-        const Tile tl = tile_of(g / NST);
-        const int s = (int)(g % NST);
-        const int8_t* src = (ldA ? a.Adig + (uint64_t)tl.l * a.adL : a.Bdig + (uint64_t)tl.l * a.D * Pcols * KK) +
-                            (uint64_t)(ldA ? tl.mb : tl.pb) * 32 + li * 16;
-        int8_t* dst = lds + (g & (NSLOT - 1)) * STAGE + wbase;
-#pragma unroll
-        for (int i = 0; i < D; ++i)
-            __builtin_amdgcn_global_load_lds((const void*)(src + i * pstride + (uint64_t)s * kstride),
-                                             (lds_ptr_t)(dst + i * PANEL), 16, 0, 0);
-    };
-    auto barrier = []() { asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory"); };
-    auto wait_next = [&](uint32_t g) {   // stage g + 1 landed: newer are the stages issued after it
-        const uint32_t last = g + 3 < G ? g + 3 : G - 1;
-        const uint32_t newer = last - (g + 1);
-        if (newer >= 2) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(2 * D) : "memory");
-        else if (newer == 1) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(D) : "memory");
-        else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    };
-    v16i acc[NS];
-#pragma unroll
-    for (int k = 0; k < NS; ++k) acc[k] = v16i{0};
-    for (uint32_t g = 0; g < 3 && g < G; ++g) issue(g);
-    if (G >= 3) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(2 * D) : "memory");   // stage 0 (1, 2 in flight)
-    else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    barrier();
-    for (uint32_t g = 0; g < G; ++g) {
-        if (g + 3 < G) issue(g + 3);
-        const int8_t* st = lds + (g & (NSLOT - 1)) * STAGE;
-        v4i bv[D];
-#pragma unroll
-        for (int j = 0; j < D; ++j) bv[j] = *(const v4i*)(st + (D + j) * PANEL + (wp + r) * 32 + 16 * h);
-#pragma unroll
-        for (int i = 0; i < D; ++i) {
-            const v4i av = *(const v4i*)(st + i * PANEL + (wm + r) * 32 + 16 * h);
-#pragma unroll
-            for (int j = 0; j < D; ++j)
-                acc[i + j] = __builtin_amdgcn_mfma_i32_32x32x32_i8(av, bv[j], acc[i + j], 0, 0, 0);
-        }
-        if (g % NST == NST - 1) {   // the tile's last stage: epilogue while the next tile's first stages land
-            const Tile tl = tile_of(g / NST);
-            mfma_epilogue<D, FAC>(a, acc, tl.l, tl.mb + wm, (uint32_t)(tl.pb + wp), r, h, Ppad);
-#pragma unroll
-            for (int k = 0; k < NS; ++k) acc[k] = v16i{0};
-        }
-        if (g + 1 < G) {
-            wait_next(g);
-            barrier();
-        }
-    }
-}
-
-static int gemm_num_cus() {
-    static int n = 0;
-    if (n == 0) {
-        int dev = 0, v = 0;
-        if (hipGetDevice(&dev) != hipSuccess || hipDeviceGetAttribute(&v, hipDeviceAttributeMultiprocessorCount, dev) !=
-                                                     hipSuccess || v < 1)
-            v = 256;
-        n = v;
-    }
-    return n;
-}
-
-template <int D, bool FAC>
-static void launch_pring(const ModGemmArgs& a, uint32_t Ppad, int l0, int nl, hipStream_t s) {
-    const uint32_t Pcols = FAC ? 2 * Ppad : Ppad;
-    const uint32_t gx = Pcols / 64, gy = (FAC ? FK : 512) / 64, ntiles = gx * gy * (uint32_t)nl;
-    static int occ = 0;
-    if (occ == 0) {
-        int o = 0;
-        if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&o, mod_gemm_mfma_pring_kernel<D, FAC>, 256, 0) != hipSuccess ||
-            o < 1)
-            o = 1;
-        occ = o;
-    }
-    const uint32_t grid = std::min<uint32_t>(ntiles, (uint32_t)(occ * gemm_num_cus()));
-    hipLaunchKernelGGL((mod_gemm_mfma_pring_kernel<D, FAC>), dim3(grid), dim3(256), 0, s, a, Ppad, l0, gx, gy, ntiles);
-}
-
-// dense launches on the persistent ring up to D = 6 (at D >= 7 its registers spill): the two-stage kernel above that
-template <int D>
-static void launch_dense_pring(const ModGemmArgs& a, uint32_t Ppad, int l0, int nl, dim3 grid, hipStream_t s) {
-    if constexpr (D <= 6) launch_pring<D, false>(a, Ppad, l0, nl, s);
-    else hipLaunchKernelGGL((mod_gemm_mfma_lds_kernel<D, false>), grid, dim3(256), 0, s, a, Ppad, l0);
-}
-
 size_t mod_gemm_mfma_ws(uint32_t P, int L, int D) {
     const uint64_t Ppad = ((uint64_t)P + 63) / 64 * 64;
     return (size_t)L * D * Ppad * MK + (size_t)L * 2 * Ppad * 8;   // digit planes, then the factored d0
@@ -852,10 +724,7 @@ static int launch_factored(const ModGemmArgs& a, int L, hipStream_t s) {
         int l1 = l0 + 1;
         while (l1 < L && (a.limbD ? std::max(a.limbD[l1], 5) : a.D) == d) ++l1;
         const dim3 grid(2 * Ppad / 64, FK / 64, l1 - l0);
-        if (a.pipe == 4) {
-            if (d == 5) launch_pring<5, true>(f, Ppad, l0, l1 - l0, s);
-            else launch_pring<6, true>(f, Ppad, l0, l1 - l0, s);
-        } else if (a.pipe == 3) {
+        if (a.pipe == 3) {
             if (d == 5) hipLaunchKernelGGL((mod_gemm_mfma_ring_kernel<5, true, true>), grid, dim3(256), 0, s, f, Ppad, l0);
             else hipLaunchKernelGGL((mod_gemm_mfma_ring_kernel<6, true, true>), grid, dim3(256), 0, s, f, Ppad, l0);
         } else if (a.pipe != 1) {   // 0 (auto) and 2: the ring (K = 256: four 64-k stages leave the fill exposed)
@@ -903,8 +772,7 @@ int launch_mod_gemm(const ModGemmArgs& a, int L, hipStream_t s) {
             switch (d) {
 #define MFHE_MFMA_CASE(dd)                                                                                    \
     case dd:                                                                                                  \
-        if (a.lds_stage && a.pipe == 4) launch_dense_pring<dd>(a, Ppad, l0, l1 - l0, grid, s);                 \
-        else if (a.lds_stage && a.pipe == 3)                                                                  \
+        if (a.lds_stage && a.pipe == 3)                                                                       \
             hipLaunchKernelGGL((mod_gemm_mfma_ring_kernel<dd, false, (dd <= 5)>), grid, dim3(256), 0, s, a, Ppad, l0); \
         else if (a.lds_stage && a.pipe == 2)                                                                  \
             hipLaunchKernelGGL((mod_gemm_mfma_ring_kernel<dd, false, false>), grid, dim3(256), 0, s, a, Ppad, l0); \
