@@ -279,6 +279,32 @@ def test_encrypt_decrypt_vs_oracle(mfhe, orc, small):
     # which can move llround at a .5 boundary): require >= 99.999 % exact agreement
     assert np.mean(gre[:words] != ore[:words]) < 1e-5
     assert np.mean(gim[:words] != oim[:words]) < 1e-5
+    # ... and exactly: b differs from the oracle's only by the W-CRT image of a noise difference (b is linear in
+    # e), so the oracle's inverse W-CRT of (b_dev - b_orc) must be a noise difference in {-1, 0, +1}, the same
+    # integer in every limb, nonzero only where the unrounded Box-Muller sample sits on a .5 rounding boundary
+    # (HE.cu:605-627: the only step where device libm and glibc may differ)
+    n2, Lq = n * n, len(RNS)
+    q_el = np.array(RNS, dtype=object)[(np.arange(words) // n2) % Lq]
+    q3 = np.array(RNS, np.uint64)[None, :, None]
+    noise = []
+    for got, want in ((gre, ore), (gim, oim)):
+        d = ((got[:words].astype(object) - want[:words].astype(object)) % q_el).astype(np.uint64)
+        poly, de = np.zeros_like(d), np.zeros_like(d)
+        orc.L.orc_matrix_to_poly(P(d), P(poly), n, Lq, 512)
+        orc.L.orc_wntt_inverse_matrix(P(poly), P(de), n, Lq, 512, P(U64(RNS)), orc.L.orc_he_VinvT(h.h))
+        de = de.reshape(512, Lq, n2)
+        sgn = np.where(de == 0, 0, np.where(de == 1, 1, np.where(de == q3 - 1, -1, 99)))
+        assert (sgn != 99).all(), "ciphertexts differ by more than a +-1 noise step"
+        assert (sgn == sgn[:, :1, :]).all(), "noise difference not the same integer in every limb"
+        noise.append(sgn[:, 0, :])
+    np.testing.assert_array_equal(noise[0], noise[1])   # re and im share e (HE.cu:605-608)
+    for w, pos in zip(*np.nonzero(noise[0])):
+        r1 = orc.L.orc_splitmix64(0xD6E8FEB86659FD93 ^ int(w * n2 + pos))
+        r2 = orc.L.orc_splitmix64(r1)
+        u1 = ((r1 >> 11) + 1.0) / 9007199254740992.0
+        u2 = ((r2 >> 11) + 1.0) / 9007199254740992.0
+        z = 3.2 * np.sqrt(-2.0 * np.log(u1)) * np.cos(6.283185307179586 * u2)
+        assert abs(abs(z) % 1.0 - 0.5) < 1e-9, (w, pos, z)
     # decrypt on identical inputs is exact
     ev = torch.empty(words, dtype=torch.int64, device="cuda")
     ctx.decrypt_to_eval(cre, sk, ev)

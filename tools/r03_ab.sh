@@ -10,7 +10,7 @@ cd "$ROOT"
 for rep in 1 2 3; do
 for v in "$@"; do
   if [ "$v" = base ]; then lib=$ROOT/matrix-fhe-gpu_amd/libmfhe.so; else lib=$ROOT/matrix-fhe-gpu_amd/libmfhe_$v.so; fi
-  NTTP_BITS=$BITS MFHE_LIB=$lib timeout -k 10 120 python tools/u64_prof.py 10 > "$OUT/$v.$rep.json" 2>&1 \
+  NTTP_BITS=$BITS NTTP_SHAPE=${NTTP_SHAPE:-16,8,1024} MFHE_LIB=$lib timeout -k 10 120 python tools/u64_prof.py 10 > "$OUT/$v.$rep.json" 2>&1 \
       || { echo "$v failed"; tail -3 "$OUT/$v.$rep.json"; exit 3; }
   echo "$v $rep $(tail -1 "$OUT/$v.$rep.json")"
 done

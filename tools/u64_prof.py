@@ -14,7 +14,7 @@ import mfhe  # noqa: E402
 from bench import gen_moduli  # noqa: E402
 
 reps = int(sys.argv[1]) if len(sys.argv) > 1 else 10
-log_n, L, batch = 16, 8, 1024
+log_n, L, batch = (int(v) for v in os.environ.get("NTTP_SHAPE", "16,8,1024").split(","))   # C3 unless set
 N = 1 << log_n
 moduli = gen_moduli(int(os.environ.get("NTTP_BITS", 60)), 1 << (log_n + 2), L)
 ctx = mfhe.Context(moduli, log_n, mfhe.CONV_PHANTOM)
