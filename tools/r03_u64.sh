@@ -1,5 +1,5 @@
 #!/bin/bash
-# One gpurun session: fused-NTT stress (mode 2 with nt outputs, mode 1 as shipped; small and C3 shapes) -> GPU
+# One gpurun session: fused-NTT stress (mode 1; small and C3 shapes) -> GPU
 # parity tests -> bench (all lines, incl. the U64 C3 line) -> two-pass floor microbenchmark.  Each GPU step has
 # its own limit; stop at the first failure.
 # usage: tools/r03_u64.sh <tag>
@@ -9,7 +9,7 @@ ROOT=${GRAFT_REPO_ROOT:-$(pwd)}
 OUT=$ROOT/gpurun_out/$TAG
 mkdir -p "$OUT"
 cd "$ROOT"
-for M in 2 1; do
+for M in 1; do
   FD_BATCH=9 FD_L=4 timeout -k 10 150 python tools/fused_diag.py $M 2 7,4 0 300 > "$OUT/stress_small_m$M.txt" 2>&1; rc=$?
   cat "$OUT/stress_small_m$M.txt"; [ $rc -ne 0 ] && exit $rc
   timeout -k 10 200 python tools/fused_diag.py $M 2 6,12 20 100 > "$OUT/stress_c3_m$M.txt" 2>&1; rc=$?
