@@ -18,6 +18,7 @@ import json
 import os
 import sys
 import time
+import traceback
 from pathlib import Path
 
 ROOT = Path(__file__).resolve().parent
@@ -679,52 +680,56 @@ def main():
         res["crt_ev_ms"], res["crt_batch"] = ev_c, cb
 
     if args.only in ("all", "recombine") and args.recombine_batch and L % world == 0:
-        # residue sharding: rank g owns limbs [g*L/G, (g+1)*L/G) of every poly.  One step =
-        # forward + inverse NTT of the shard (a computation round trip) + RCCL exchange + sharded CRT
-        # compose of this rank's batch slice -> f64.  The shard holds RNS residues of real messages
-        # (|z| < 1 scaled by delta), as a decode does.
-        from mfhe import dist as mdist
-        rb = max(world, args.recombine_batch // world * world)
-        s0, lg = mdist.limb_range(L, world, rank)
-        full = torch.empty(rb * L * N, dtype=torch.int64, device=dev)
-        zr = torch.rand(rb * N, dtype=torch.float64, device=dev, generator=g) * 2 - 1
-        ctx.rns_decompose(zr, full, rb, N, stream=stream)
-        shard = full.view(rb, L, N)[:, s0:s0 + lg, :].contiguous().view(-1)
-        del full, zr
-        rout = torch.empty(rb // world * N, dtype=torch.float64, device=dev)
-        # multi-GPU: the recombine is the native RCCL call (mfhe_crt_recombine_sharded) on a communicator
-        # owned by libmfhe, receive buffers reserved here, outside the timed steps
-        comm = None
-        if world > 1 and backend == "nccl":
-            comm = mfhe.Comm.create()
-            for mode in ("allgather", "alltoall"):
-                ctx.crt_recombine_reserve(comm, mode, rb, N)
-        rc = {}
-        nrep = max(1, args.steps // 4)
-        modes = ("allgather", "alltoall") if world > 1 else ("local",)
-        for mode in modes:
-            def step(mode=mode):
+        try:
+            # residue sharding: rank g owns limbs [g*L/G, (g+1)*L/G) of every poly.  One step =
+            # forward + inverse NTT of the shard (a computation round trip) + RCCL exchange + sharded CRT
+            # compose of this rank's batch slice -> f64.  The shard holds RNS residues of real messages
+            # (|z| < 1 scaled by delta), as a decode does.
+            from mfhe import dist as mdist
+            rb = max(world, args.recombine_batch // world * world)
+            s0, lg = mdist.limb_range(L, world, rank)
+            full = torch.empty(rb * L * N, dtype=torch.int64, device=dev)
+            zr = torch.rand(rb * N, dtype=torch.float64, device=dev, generator=g) * 2 - 1
+            ctx.rns_decompose(zr, full, rb, N, stream=stream)
+            shard = full.view(rb, L, N)[:, s0:s0 + lg, :].contiguous().view(-1)
+            del full, zr
+            rout = torch.empty(rb // world * N, dtype=torch.float64, device=dev)
+            # multi-GPU: the recombine is the native RCCL call (mfhe_crt_recombine_sharded) on a communicator
+            # owned by libmfhe, receive buffers reserved here, outside the timed steps
+            comm = None
+            if world > 1 and backend == "nccl":
+                comm = mfhe.Comm.create()
+                for mode in ("allgather", "alltoall"):
+                    ctx.crt_recombine_reserve(comm, mode, rb, N)
+            rc = {}
+            nrep = max(1, args.steps // 4)
+            modes = ("allgather", "alltoall") if world > 1 else ("local",)
+            for mode in modes:
+                def step(mode=mode):
+                    ctx.ntt_fwd(shard, batch=rb, start_limb=s0, nlimbs=lg, stream=stream)
+                    ctx.ntt_inv(shard, batch=rb, start_limb=s0, nlimbs=lg, stream=stream)
+                    if mode == "local":
+                        ctx.crt_compose_f64(shard, rout, rb, N, stream=stream)
+                    else:
+                        mdist.crt_recombine(ctx, shard, rb, N, mode, out=rout, stream=stream, comm=comm)
+                w_r, _ = timed(step, nrep, 1)
+                rc[mode] = w_r / nrep
+
+            def ntt_rt():
                 ctx.ntt_fwd(shard, batch=rb, start_limb=s0, nlimbs=lg, stream=stream)
                 ctx.ntt_inv(shard, batch=rb, start_limb=s0, nlimbs=lg, stream=stream)
-                if mode == "local":
-                    ctx.crt_compose_f64(shard, rout, rb, N, stream=stream)
-                else:
-                    mdist.crt_recombine(ctx, shard, rb, N, mode, out=rout, stream=stream, comm=comm)
-            w_r, _ = timed(step, nrep, 1)
-            rc[mode] = w_r / nrep
-
-        def ntt_rt():
-            ctx.ntt_fwd(shard, batch=rb, start_limb=s0, nlimbs=lg, stream=stream)
-            ctx.ntt_inv(shard, batch=rb, start_limb=s0, nlimbs=lg, stream=stream)
-        w_n, _ = timed(ntt_rt, nrep, 1)
-        if comm is not None:
-            comm.close()
-        res["recombine"] = {"batch": rb, "limbs_per_gpu": lg, "ntt_roundtrip_only_ms": w_n / nrep * 1e3,
-                            "exchange": ("none (1 GPU: local compose)" if world == 1 else "native RCCL (mfhe_crt_recombine_sharded)")
-                                        if comm is not None or world == 1
-                                        else "torch.distributed " + backend,
-                            **{f"{m}_ms": t * 1e3 for m, t in rc.items()},
-                            **{f"{m}_polys_per_s": rb / t for m, t in rc.items()}}
+            w_n, _ = timed(ntt_rt, nrep, 1)
+            if comm is not None:
+                comm.close()
+            res["recombine"] = {"batch": rb, "limbs_per_gpu": lg, "ntt_roundtrip_only_ms": w_n / nrep * 1e3,
+                                "exchange": ("none (1 GPU: local compose)" if world == 1 else "native RCCL (mfhe_crt_recombine_sharded)")
+                                            if comm is not None or world == 1
+                                            else "torch.distributed " + backend,
+                                **{f"{m}_ms": t * 1e3 for m, t in rc.items()},
+                                **{f"{m}_polys_per_s": rb / t for m, t in rc.items()}}
+        except Exception as e:   # a secondary line must not cost the headline line
+            traceback.print_exc()
+            res["recombine"] = {"error": repr(e)[:300]}
 
     c4 = None
     if args.only in ("all", "c4") and not args.no_pipeline:
@@ -733,12 +738,20 @@ def main():
         else:
             c4comm = mfhe.Comm.from_id(mfhe.Comm.unique_id(), 1, 0) if world == 1 else None
         if c4comm is not None:
-            c4 = c4_line(world, rank, c4comm, barrier)
+            try:
+                c4 = c4_line(world, rank, c4comm, barrier)
+            except Exception as e:   # a secondary line must not cost the headline line
+                traceback.print_exc()
+                c4 = {"error": repr(e)[:300]}
             c4comm.close()
 
     c5 = None
     if args.only in ("all", "c5") and not args.no_c5:
-        c5 = c5_line(world, rank, barrier, timed, backend)
+        try:
+            c5 = c5_line(world, rank, barrier, timed, backend)
+        except Exception as e:   # a secondary line must not cost the headline line
+            traceback.print_exc()
+            c5 = {"error": repr(e)[:300]}
         torch.cuda.empty_cache()
 
     if rank == 0:
