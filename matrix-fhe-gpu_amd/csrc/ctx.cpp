@@ -331,6 +331,63 @@ static int build_wcrt(mfhe_ctx* c) {
                         }
                 }
                 if ((rc = upload(c, &c->d_wZdig, zd)) || (rc = upload(c, &c->d_wfold, fo))) return rc;
+                // factored inverse (gemm.hip mfma_digitize_ifold_kernel / epilogue): the 771-point interpolation
+                // with zeros at the non-units, reduced mod Phi_771 (tools/wcrt_factor_check.py).  Zi[i][k] =
+                // zeta^-((i+1)(k+1)); kappa[a][t] = 771^-1 omega^(-a t); lam1[a][t] = kappa[a][t] - kappa[a][t+1],
+                // lam2[a][t] = kappa[a][t+2] - kappa[a][t+1] (t mod 3); z[l][0 / 1][k] = zeta^(-255 / -256 (k+1)).
+                std::vector<int8_t> zid((size_t)L * D * FK * FK);
+                std::vector<double> ifo((size_t)L * 16, 0.0), iz((size_t)L * 2 * FK);
+                for (int l = 0; l < L; ++l) {
+                    const uint64_t q = c->moduli[l], eta = hm::find_eta771(q);
+                    const uint64_t zinv = hm::powmod(hm::powmod(eta, 3, q), 256, q), omega = hm::powmod(eta, 257, q);
+                    const uint64_t inv771 = hm::powmod(771 % q, q - 2, q);
+                    int8_t d[8];
+                    for (int i = 0; i < FK; ++i) {
+                        const uint64_t zi = hm::powmod(zinv, (uint64_t)i + 1, q);
+                        uint64_t cur = zi;
+                        for (int k = 0; k < FK; ++k, cur = hm::mulmod(cur, zi, q)) {
+                            balanced_digits(cur, D, d);
+                            const size_t o = ((size_t)(k >> 5) * FK + i) * 32 + (k & 31);
+                            for (int j = 0; j < D; ++j) zid[((size_t)l * D + j) * FK * FK + o] = d[j];
+                        }
+                    }
+                    uint64_t kap[2][3];
+                    for (int ap = 0; ap < 2; ++ap)
+                        for (int t = 0; t < 3; ++t)
+                            kap[ap][t] = hm::mulmod(inv771, hm::powmod(omega, (uint64_t)((3 - ((ap + 1) * t) % 3) % 3), q), q);
+                    auto sub = [q](uint64_t x, uint64_t y) { return x >= y ? x - y : x + q - y; };
+                    ifo[(size_t)l * 16 + 0] = (double)q;
+                    ifo[(size_t)l * 16 + 1] = 1.0 / (double)q;
+                    for (int ap = 0; ap < 2; ++ap)
+                        for (int t = 0; t < 3; ++t) {
+                            ifo[(size_t)l * 16 + 2 + 3 * ap + t] = centred(sub(kap[ap][t], kap[ap][(t + 1) % 3]), q);
+                            ifo[(size_t)l * 16 + 8 + 3 * ap + t] = centred(sub(kap[ap][(t + 2) % 3], kap[ap][(t + 1) % 3]), q);
+                        }
+                    for (int s = 0; s < 2; ++s) {
+                        const uint64_t zs = hm::powmod(zinv, 255 + (uint64_t)s, q);
+                        uint64_t cur = zs;
+                        for (int k = 0; k < FK; ++k, cur = hm::mulmod(cur, zs, q))
+                            iz[((size_t)l * 2 + s) * FK + k] = centred(cur, q);
+                    }
+                }
+                // Phi_771 = (x^514 + x^257 + 1) / (x^2 + x + 1), coefficients in {-1, 0, 1}; phi[j + 1] = coefficient j
+                std::vector<int> num(515, 0), ph(513, 0);
+                num[0] = num[257] = num[514] = 1;
+                for (int d = 514; d >= 2; --d)
+                    if (num[d]) {
+                        const int cf = num[d];
+                        ph[d - 2] = cf;
+                        num[d] -= cf;
+                        num[d - 1] -= cf;
+                        num[d - 2] -= cf;
+                    }
+                auto pc = [&](int j) { return (uint8_t)((j < 0 ? 0 : ph[j]) + 1); };
+                std::vector<uint8_t> phi(320, 0);
+                for (int r2 = 0; r2 <= 256; ++r2)
+                    phi[r2 ? r2 - 1 : 256] = (uint8_t)(pc(r2) | pc(r2 - 1) << 2 | pc(r2 + 257) << 4 | pc(r2 + 256) << 6);
+                if ((rc = upload(c, &c->d_wZidig, zid)) || (rc = upload(c, &c->d_wifold, ifo)) ||
+                    (rc = upload(c, &c->d_wiz, iz)) || (rc = upload(c, &c->d_wphi, phi)))
+                    return rc;
             }
         }
     }

@@ -317,7 +317,8 @@ __global__ __launch_bounds__(256) void mfma_digitize_kernel(const uint64_t* __re
         for (int c = 0; c < 8; ++c) pk[i][c] = 0;
 #pragma unroll
     for (int kk = 0; kk < 32; ++kk) {
-        uint64_t x = p < P ? Bl[(uint64_t)(kc * 32 + kk) * sbK + col] : 0;
+        uint64_t x = Bl[(uint64_t)(kc * 32 + kk) * sbK + (p < P ? col : 0)];
+        x = p < P ? x : 0;
 #pragma unroll
         for (int i = 0; i < D; ++i) {
             const uint32_t v = (uint32_t)x & 255u;
@@ -380,7 +381,10 @@ __global__ __launch_bounds__(256) void mfma_digitize_fold_kernel(const uint64_t*
     const uint64_t* Bl = B + (uint64_t)l * bL;
     const uint64_t col = (uint64_t)(p >> log_n) * sbY + (p & ((1u << log_n) - 1));
     const bool live = p < P;
-    auto in = [&](int r) { return live ? ArithF64::from_u64(Bl[(uint64_t)r * sbK + col]) : 0.0; };
+    // unconditional loads (column 0 stands in for the padding columns, then zeroed): a load under `live ? :` is
+    // a branch per load, each followed by its own vmcnt(0) -- the 32 loads of a thread ran one at a time
+    const uint64_t cl = live ? col : 0;
+    auto in = [&](int r) { const double x = ArithF64::from_u64(Bl[(uint64_t)r * sbK + cl]); return live ? x : 0.0; };
     uint32_t pk[2][D][4];
 #pragma unroll
     for (int ap = 0; ap < 2; ++ap)
@@ -393,7 +397,7 @@ __global__ __launch_bounds__(256) void mfma_digitize_fold_kernel(const uint64_t*
 #pragma unroll
     for (int kk = 0; kk < 16; ++kk) {
         const int r2 = rb + kk;
-        const double x1 = in(r2), x2 = r2 + 257 < 512 ? in(r2 + 257) : 0.0;
+        const double x1 = in(r2), x2r = in(r2 + 257 < 512 ? r2 + 257 : 511), x2 = r2 + 257 < 512 ? x2r : 0.0;
 #pragma unroll
         for (int ap = 0; ap < 2; ++ap) {
             const double w1 = r1 == 0 ? c1[ap][0] : (r1 == 1 ? c1[ap][1] : c1[ap][2]);
@@ -428,13 +432,221 @@ __global__ __launch_bounds__(256) void mfma_digitize_fold_kernel(const uint64_t*
         }
 }
 
+// ---- factored inverse W-CRT (every q < 2^50; tools/wcrt_factor_check.py) ----
+// V^-1 y is the 771-point inverse DFT of the 512 values (zeros at the 259 non-unit exponents), reduced mod
+// Phi_771.  With the forward's e = 257 a + 3 b order, E_a[r2] = sum_{b=1..256} zeta^(-b r2) y[a][b] (r2 = 0..256) and
+//   g_r = 771^-1 sum_a omega^(-a r) E_a[r mod 257]                       (r = 0..770)
+//   h_j = g_j - g_(j+514) (j <= 256),  h_j = g_j - g_(j+257) (257 <= j <= 513)   (mod x^514 + x^257 + 1)
+//   f_j = h_j - c0 phi_j - c1 phi_(j-1),  c1 = h_513, c0 = h_512 - c1 phi_511       (mod Phi_771, j < 512)
+// j = r2, r2 + 257 and r2 + 514 share E_a[r2], so per GEMM row r2 = 1..256 (a 256 x 256 GEMM over 2 P columns
+// interleaved as 2 p + a'): h_r2 = sum_a lam1[a][r2 mod 3] E_a[r2], h_(r2+257) = sum_a lam2[a][r2 mod 3] E_a[r2].
+// The digitize kernel below also forms the rows r2 = 0 (-> f_0, f_257), 255 and 256 (-> c0, c1 per column) by
+// dot products, so the GEMM epilogue writes the final f directly: half the MACs of the dense V^-1 product.
+// One thread: column p = 16 blockIdx.x + lane / 4, a' = (lane >> 1) & 1, half panel hf = lane & 1 (16 k), k quarter
+// = wave (two 32-k panels): lane l's 16-byte digit store lands at byte 16 l of a contiguous 1 KiB run.
+template <int D>
+__global__ __launch_bounds__(256) void mfma_digitize_ifold_kernel(ModGemmArgs a, uint32_t Ppad, PlaneCounts pc) {
+    __shared__ double red[3][4][64];
+    __shared__ double z[2 * FK];   // the limb's dot-product rows zeta^(-255 b), zeta^(-256 b)
+    const int lane = threadIdx.x & 63, kq = threadIdx.x >> 6;
+    const uint32_t p = blockIdx.x * 16 + (lane >> 2);
+    const int ap = (lane >> 1) & 1, hf = lane & 1;
+    const int l = blockIdx.y;
+    typedef const __attribute__((address_space(4))) double* cdp_t;
+    const cdp_t fo = (cdp_t)(a.ifold + (uint64_t)l * 16);
+    LimbConst lc;
+    lc.qf = fo[0];
+    lc.qinv = fo[1];
+    const ArithF64 ar(lc);
+    z[threadIdx.x] = a.iz[(uint64_t)l * 2 * FK + threadIdx.x];
+    z[threadIdx.x + 256] = a.iz[(uint64_t)l * 2 * FK + 256 + threadIdx.x];
+    __syncthreads();
+    const uint64_t* Bl = a.B + (uint64_t)l * a.bL;
+    const uint32_t nmask = (1u << a.log_n) - 1;
+    const uint64_t col = (uint64_t)(p >> a.log_n) * a.sbY + (p & nmask);
+    const bool live = p < a.P;
+    const uint64_t cl = live ? col : 0;   // unconditional loads (see mfma_digitize_fold_kernel)
+    const int nd = l < 64 ? pc.n[l] : D;
+    double s0 = 0.0, s1 = 0.0, s2 = 0.0;   // E_a'[0], E_a'[255], E_a'[256] over this thread's 32 k
+#pragma unroll 1
+    for (int pn = 0; pn < 2; ++pn) {
+        const int kc = 2 * kq + pn, k0 = kc * 32 + hf * 16;
+        uint32_t pk[D][4];
+#pragma unroll
+        for (int i = 0; i < D; ++i)
+#pragma unroll
+            for (int c = 0; c < 4; ++c) pk[i][c] = 0;
+        double v[16];
+#pragma unroll
+        for (int kk = 0; kk < 16; ++kk)   // b = k0 + kk + 1
+            v[kk] = ArithF64::from_u64(Bl[(uint64_t)(ap * FK + k0 + kk) * a.sbK + cl]);
+#pragma unroll
+        for (int kk = 0; kk < 16; ++kk) v[kk] = live ? ar.reduce(v[kk]) : 0.0;
+        // the three dot products as two independent chains each (exact: |partial| < 9 q < 2^54 is never reached,
+        // every chain is re-centred after 4 terms)
+        double t0[2] = {0.0, 0.0}, t1[2] = {0.0, 0.0}, t2[2] = {0.0, 0.0};
+#pragma unroll
+        for (int kk = 0; kk < 16; ++kk) {
+            const int c = kk & 1;
+            t0[c] += v[kk];
+            t1[c] += ar.mulmod(v[kk], z[k0 + kk]);
+            t2[c] += ar.mulmod(v[kk], z[FK + k0 + kk]);
+            if ((kk & 7) >= 6) {
+                t0[c] = ar.reduce(t0[c]);
+                t1[c] = ar.reduce(t1[c]);
+                t2[c] = ar.reduce(t2[c]);
+            }
+            const uint64_t y = balanced_bytes<D>(v[kk]);
+            const uint32_t lo = (uint32_t)y, hi = (uint32_t)(y >> 32);
+#pragma unroll
+            for (int i = 0; i < D; ++i) {
+                const uint32_t b = i < 4 ? (lo >> (8 * i)) & 255u : (hi >> (8 * (i - 4))) & 255u;
+                pk[i][kk >> 2] |= b << (8 * (kk & 3));
+            }
+        }
+        s0 = ar.reduce(s0 + t0[0] + t0[1]);
+        s1 = ar.reduce(s1 + t1[0] + t1[1]);
+        s2 = ar.reduce(s2 + t2[0] + t2[1]);
+#pragma unroll
+        for (int i = 0; i < D; ++i) {
+            if (i >= nd) break;
+            int8_t* o = a.Bdig + (((uint64_t)l * D + i) * (FK / 32) + kc) * 2 * Ppad * 32 + (uint64_t)blockIdx.x * 1024 +
+                        lane * 16;
+            const uint32_t* w = pk[i];
+            *(v4i*)o = v4i{(int)(w[0] ^ 0x80808080u), (int)(w[1] ^ 0x80808080u), (int)(w[2] ^ 0x80808080u),
+                           (int)(w[3] ^ 0x80808080u)};
+        }
+    }
+    // halves of a panel -> lanes l, l ^ 1; quarters -> the four waves (LDS); a' -> lanes l, l ^ 2
+    s0 += __shfl_xor(s0, 1);
+    s1 += __shfl_xor(s1, 1);
+    s2 += __shfl_xor(s2, 1);
+    red[0][kq][lane] = s0;
+    red[1][kq][lane] = s1;
+    red[2][kq][lane] = s2;
+    __syncthreads();
+    if (kq != 0) return;   // wave 0 finishes (no barrier below)
+    double e[3];
+#pragma unroll
+    for (int t = 0; t < 3; ++t) e[t] = ar.reduce(red[t][0][lane] + red[t][1][lane] + red[t][2][lane] + red[t][3][lane]);
+    double o[3];
+#pragma unroll
+    for (int t = 0; t < 3; ++t) o[t] = __shfl_xor(e[t], 2);
+    const double e1[3] = {ap ? o[0] : e[0], ap ? o[1] : e[1], ap ? o[2] : e[2]};   // a = 1
+    const double e2[3] = {ap ? e[0] : o[0], ap ? e[1] : o[1], ap ? e[2] : o[2]};   // a = 2
+    // fo[2 + 3 a' + t] = lam1[a'][t], fo[8 + 3 a' + t] = lam2[a'][t]
+    const double h0 = ar.mulmod(e1[0], fo[2]) + ar.mulmod(e2[0], fo[5]);          // r2 = 0, t = 0
+    const double h257 = ar.mulmod(e1[0], fo[8]) + ar.mulmod(e2[0], fo[11]);
+    const double h512 = ar.mulmod(e1[1], fo[8]) + ar.mulmod(e2[1], fo[11]);       // r2 = 255, t = 0
+    const double h513 = ar.mulmod(e1[2], fo[9]) + ar.mulmod(e2[2], fo[12]);       // r2 = 256, t = 1
+    // packed Phi_771 rows (mfhe_ctx::d_wphi): byte r2 - 1 (r2 = 1..256; r2 = 0 at byte 256) holds phi_r2, phi_(r2-1),
+    // phi_(r2+257), phi_(r2+256) as 2-bit fields (value + 1) at shifts 0, 2, 4, 6
+    auto phi = [&](int byte, int sh) { return (double)((int)((a.phi[byte] >> sh) & 3) - 1); };
+    const double c1 = ar.reduce(h513);
+    const double c0 = ar.reduce(h512 - c1 * phi(254, 6));   // phi_511 = phi_(r2+256) at r2 = 255
+    if (!live || hf) return;
+    uint64_t* Cl = a.C + (uint64_t)l * a.cL + (uint64_t)(p >> a.log_n) * a.scY + (p & nmask);
+    if (ap == 0) {
+        Cl[0] = ar.canon(h0 - c0 * phi(256, 0));
+        a.cc[((uint64_t)l * Ppad + p) * 2] = c0;
+        a.cc[((uint64_t)l * Ppad + p) * 2 + 1] = c1;
+    } else {
+        Cl[257 * a.scM] = ar.canon(h257 - c0 * phi(256, 4) - c1 * phi(256, 6));
+    }
+}
+
 // C = sum_s acc_s * 256^s mod q for the 32 x 32 wave tile at (m0, p0) of limb l (lane = (r, h)).
-// FAC: factored forward -- column p0 + r is (a', p) = divmod(., Ppad), output row a' * 256 + row, plus d0.
-template <int D, bool FAC = false>
+// MODE 1 (factored forward): column p0 + r is (a', p) = divmod(., Ppad), output row a' * 256 + row, plus d0.
+// MODE 2 (factored inverse): column p0 + r is 2 p + a', row r2 - 1; lanes r, r ^ 1 hold a' = 0, 1 of one column
+// and trade their lam products, then write f_r2 (a' = 0) and f_(r2+257) (a' = 1, r2 <= 254).
+// lanes l <-> l ^ 1 (DPP quad_perm [1, 0, 3, 2]: a VALU move, no LDS crossbar)
+__device__ __forceinline__ double swap_pair(double x) {
+    const int lo = __double2loint(x), hi = __double2hiint(x);
+    return __hiloint2double(__builtin_amdgcn_mov_dpp(hi, 0xB1, 0xF, 0xF, true),
+                            __builtin_amdgcn_mov_dpp(lo, 0xB1, 0xF, 0xF, true));
+}
+
+// MODE 2: this lane's column's (c0, c1), loaded before the K loop so the epilogue does not wait for them
+struct InvCC {
+    double c0 = 0.0, c1 = 0.0;
+};
+template <int MODE>
+__device__ __forceinline__ InvCC inv_cc(const ModGemmArgs& a, int l, uint32_t p0, int r, uint32_t Ppad) {
+    InvCC c;
+    if constexpr (MODE == 2) {
+        const uint32_t p = (p0 + r) >> 1;
+        const double* src = a.cc + ((uint64_t)l * Ppad + (p < a.P ? p : 0)) * 2;
+        c.c0 = src[0];
+        c.c1 = src[1];
+    }
+    return c;
+}
+
+template <int D, int MODE = 0>
 __device__ __forceinline__ void mfma_epilogue(const ModGemmArgs& a, const v16i (&acc)[2 * D - 1], int l, int m0,
-                                              uint32_t p0, int r, int h, uint32_t Ppad = 0) {
+                                              uint32_t p0, int r, int h, uint32_t Ppad = 0, InvCC cc = InvCC{}) {
     constexpr int NS = 2 * D - 1;
+    constexpr bool FAC = MODE != 0;
     uint64_t* Cl = a.C + (uint64_t)l * a.cL;
+    if constexpr (MODE == 2) {
+        typedef const __attribute__((address_space(4))) double* cdp_t;
+        const cdp_t ep = (cdp_t)(a.epi + (uint64_t)l * 8);
+        const cdp_t fo = (cdp_t)(a.ifold + (uint64_t)l * 16);
+        LimbConst lc;
+        lc.qf = ep[0];
+        lc.qinv = ep[1];
+        const ArithF64 ar(lc);
+        const double c32[3] = {ep[2], ep[3], ep[4]};
+        const uint32_t colf = p0 + r;
+        const int ap = colf & 1;
+        const uint32_t p = colf >> 1;
+        const bool live = p < a.P;   // the same for both lanes of a pair
+        double lam1[3], lam2[3];
+#pragma unroll
+        for (int t = 0; t < 3; ++t) {
+            lam1[t] = ap ? fo[5 + t] : fo[2 + t];
+            lam2[t] = ap ? fo[11 + t] : fo[8 + t];
+        }
+        const double c0 = cc.c0, c1 = cc.c1;
+        uint64_t* Cp = Cl + (uint64_t)(p >> a.log_n) * a.scY + (p & ((1u << a.log_n) - 1));
+        // the packed Phi rows of this wave tile's 32 rows r2 = m0 + 1 .. m0 + 32 (bytes m0 .. m0 + 31) by scalar loads
+        typedef const __attribute__((address_space(4))) uint32_t* cu32_t;
+        const cu32_t pw = (cu32_t)(a.phi + m0);
+        uint32_t win[8];
+#pragma unroll
+        for (int i = 0; i < 8; ++i) win[i] = pw[i];
+        const int sh = ap ? 4 : 0;   // fields (phi_j, phi_(j-1)) of this lane's output row j
+        constexpr int NZ = (NS + 1) / 2, NY = (NZ + 1) / 2;
+#pragma unroll
+        for (int reg = 0; reg < 16; ++reg) {
+            const int r2 = m0 + (reg & 3) + 8 * (reg >> 2) + 4 * h + 1;
+            const uint32_t pb = ((h ? win[2 * (reg >> 2) + 1] : win[2 * (reg >> 2)]) >> (8 * (reg & 3) + sh)) & 15u;
+            double zz[NZ];
+#pragma unroll
+            for (int t = 0; t < NZ; ++t)
+                zz[t] = 2 * t + 1 < NS ? __fma_rn(256.0, (double)acc[2 * t + 1][reg], (double)acc[2 * t][reg])
+                                       : (double)acc[2 * t][reg];
+            double v = 0.0;
+#pragma unroll
+            for (int u = 0; u < NY; ++u) {
+                const double y = 2 * u + 1 < NZ ? __fma_rn(65536.0, zz[2 * u + 1], zz[2 * u]) : zz[2 * u];
+                v += u == 0 ? y : ar.mulmod(y, c32[u - 1]);
+            }
+            const double e = ar.reduce(v);
+            const uint32_t t = (uint32_t)r2 % 3u;
+            const double w1 = t == 0 ? lam1[0] : (t == 1 ? lam1[1] : lam1[2]);
+            const double w2 = t == 0 ? lam2[0] : (t == 1 ? lam2[1] : lam2[2]);
+            const double p1 = ar.mulmod(e, w1), p2 = ar.mulmod(e, w2);
+            const double got = swap_pair(ap ? p1 : p2);   // the partner's share of this lane's output
+            const double hv = (ap ? p2 : p1) + got;
+            const int j = ap ? r2 + 257 : r2;
+            if (live && (ap == 0 || r2 <= 254)) {
+                const double fj = hv - c0 * (double)((int)(pb & 3u) - 1) - c1 * (double)((int)(pb >> 2) - 1);
+                Cp[(uint64_t)j * a.scM] = ar.canon(fj);
+            }
+        }
+        return;
+    }
     if (FAC || a.epi) {
         // FP64 (every q < 2^50): |acc_s| < 2^26, so z_t = acc_2t + 256 acc_2t+1 (< 2^35) and
         // y_u = z_2u + 2^16 z_2u+1 (< 2^51) are exact doubles; C = y_0 + sum_u y_u (2^32u mod q), each
@@ -539,9 +751,10 @@ __global__ __launch_bounds__(256, D <= 5 ? 2 : 1) void mod_gemm_mfma_kernel(ModG
 // RAW order for the DMA'd bytes: issuing waves' s_waitcnt vmcnt(0), then the barrier, then the reads.
 typedef __attribute__((address_space(3))) void* lds_ptr_t;
 
-template <int D, bool FAC>
+template <int D, int MODE>
 __global__ __launch_bounds__(256, D <= 5 ? 2 : 1) void mod_gemm_mfma_lds_kernel(ModGemmArgs a, uint32_t Ppad, int limb0) {
-    // FAC: M = K = 256 and 2 Ppad B columns (factored forward); else M = K = 512 and Ppad columns
+    // MODE 1 / 2 (factored forward / inverse): M = K = 256 and 2 Ppad B columns; 0: M = K = 512 and Ppad columns
+    constexpr bool FAC = MODE != 0;
     constexpr int KK = FAC ? FK : MK, AM = FAC ? FK : 512;
     const uint32_t Pcols = FAC ? 2 * Ppad : Ppad;
     constexpr int NS = 2 * D - 1;
@@ -572,6 +785,7 @@ __global__ __launch_bounds__(256, D <= 5 ? 2 : 1) void mod_gemm_mfma_lds_kernel(
                                                  (lds_ptr_t)(lds + buf * STAGE + wbase + i * PLANE + pp * PANEL), 16,
                                                  0, 0);
     };
+    const InvCC icc = inv_cc<MODE>(a, l, (uint32_t)(pb + wp), r, Ppad);
     v16i acc[NS];
 #pragma unroll
     for (int s = 0; s < NS; ++s) acc[s] = v16i{0};
@@ -599,7 +813,7 @@ __global__ __launch_bounds__(256, D <= 5 ? 2 : 1) void mod_gemm_mfma_lds_kernel(
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // this wave's DMA into buf ^ 1 has landed
         __syncthreads();
     }
-    mfma_epilogue<D, FAC>(a, acc, l, mb + wm, (uint32_t)(pb + wp), r, h, Ppad);
+    mfma_epilogue<D, MODE>(a, acc, l, mb + wm, (uint32_t)(pb + wp), r, h, Ppad, icc);
 }
 
 // Ring variant (MFHE_OPT_WCRT_PIPE 2 / 3, and 0 = auto on the factored launch): the same tile, digit planes and
@@ -613,8 +827,9 @@ __global__ __launch_bounds__(256, D <= 5 ? 2 : 1) void mod_gemm_mfma_lds_kernel(
 // AHEAD: the next A fragment's LDS read is issued before the current fragment's D MFMAs (sched_barrier-pinned),
 // so its latency hides behind them instead of being waited for in front of them (D <= 5 only: at D >= 6 the
 // extra fragment spills).
-template <int D, bool FAC, bool AHEAD>
+template <int D, int MODE, bool AHEAD>
 __global__ __launch_bounds__(256, D <= 5 ? 2 : 1) void mod_gemm_mfma_ring_kernel(ModGemmArgs a, uint32_t Ppad, int limb0) {
+    constexpr bool FAC = MODE != 0;
     constexpr int KK = FAC ? FK : MK, AM = FAC ? FK : 512;
     const uint32_t Pcols = FAC ? 2 * Ppad : Ppad;
     constexpr int NS = 2 * D - 1;
@@ -644,6 +859,7 @@ __global__ __launch_bounds__(256, D <= 5 ? 2 : 1) void mod_gemm_mfma_ring_kernel
                                              (lds_ptr_t)(dst + i * PANEL), 16, 0, 0);
     };
     auto barrier = []() { asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory"); };
+    const InvCC icc = inv_cc<MODE>(a, l, (uint32_t)(pb + wp), r, Ppad);   // older than every DMA: the counted waits cover it
     v16i acc[NS];
 #pragma unroll
     for (int s = 0; s < NS; ++s) acc[s] = v16i{0};
@@ -688,7 +904,7 @@ __global__ __launch_bounds__(256, D <= 5 ? 2 : 1) void mod_gemm_mfma_ring_kernel
             barrier();
         }
     }
-    mfma_epilogue<D, FAC>(a, acc, l, mb + wm, (uint32_t)(pb + wp), r, h, Ppad);
+    mfma_epilogue<D, MODE>(a, acc, l, mb + wm, (uint32_t)(pb + wp), r, h, Ppad, icc);
 }
 
 size_t mod_gemm_mfma_ws(uint32_t P, int L, int D) {
@@ -725,14 +941,14 @@ static int launch_factored(const ModGemmArgs& a, int L, hipStream_t s) {
         while (l1 < L && (a.limbD ? std::max(a.limbD[l1], 5) : a.D) == d) ++l1;
         const dim3 grid(2 * Ppad / 64, FK / 64, l1 - l0);
         if (a.pipe == 3) {
-            if (d == 5) hipLaunchKernelGGL((mod_gemm_mfma_ring_kernel<5, true, true>), grid, dim3(256), 0, s, f, Ppad, l0);
-            else hipLaunchKernelGGL((mod_gemm_mfma_ring_kernel<6, true, true>), grid, dim3(256), 0, s, f, Ppad, l0);
+            if (d == 5) hipLaunchKernelGGL((mod_gemm_mfma_ring_kernel<5, 1, true>), grid, dim3(256), 0, s, f, Ppad, l0);
+            else hipLaunchKernelGGL((mod_gemm_mfma_ring_kernel<6, 1, true>), grid, dim3(256), 0, s, f, Ppad, l0);
         } else if (a.pipe != 1) {   // 0 (auto) and 2: the ring (K = 256: four 64-k stages leave the fill exposed)
-            if (d == 5) hipLaunchKernelGGL((mod_gemm_mfma_ring_kernel<5, true, false>), grid, dim3(256), 0, s, f, Ppad, l0);
-            else hipLaunchKernelGGL((mod_gemm_mfma_ring_kernel<6, true, false>), grid, dim3(256), 0, s, f, Ppad, l0);
+            if (d == 5) hipLaunchKernelGGL((mod_gemm_mfma_ring_kernel<5, 1, false>), grid, dim3(256), 0, s, f, Ppad, l0);
+            else hipLaunchKernelGGL((mod_gemm_mfma_ring_kernel<6, 1, false>), grid, dim3(256), 0, s, f, Ppad, l0);
         } else {
-            if (d == 5) hipLaunchKernelGGL((mod_gemm_mfma_lds_kernel<5, true>), grid, dim3(256), 0, s, f, Ppad, l0);
-            else hipLaunchKernelGGL((mod_gemm_mfma_lds_kernel<6, true>), grid, dim3(256), 0, s, f, Ppad, l0);
+            if (d == 5) hipLaunchKernelGGL((mod_gemm_mfma_lds_kernel<5, 1>), grid, dim3(256), 0, s, f, Ppad, l0);
+            else hipLaunchKernelGGL((mod_gemm_mfma_lds_kernel<6, 1>), grid, dim3(256), 0, s, f, Ppad, l0);
         }
         MFHE_CHECK_LAUNCH("mod_gemm_mfma_lds_kernel (factored)");
         l0 = l1;
@@ -740,7 +956,44 @@ static int launch_factored(const ModGemmArgs& a, int L, hipStream_t s) {
     return MFHE_OK;
 }
 
+// factored inverse: digitize (+ rows 0 / 255 / 256 by dot products), then the 256 x 256 GEMM per run of equal
+// digit counts with the MODE 2 epilogue
+static int launch_factored_inv(const ModGemmArgs& a, int L, hipStream_t s) {
+    const uint32_t Ppad = (a.P + 63) / 64 * 64;
+    ModGemmArgs f = a;
+    f.cc = (double*)(a.Bdig + (size_t)L * a.D * Ppad * MK);   // the d0 region: L * Ppad * 2 doubles
+    const dim3 gd(Ppad / 16, L);
+    const PlaneCounts pc = plane_counts(a, L);
+    if (a.D == 5) hipLaunchKernelGGL(mfma_digitize_ifold_kernel<5>, gd, dim3(256), 0, s, f, Ppad, pc);
+    else hipLaunchKernelGGL(mfma_digitize_ifold_kernel<6>, gd, dim3(256), 0, s, f, Ppad, pc);
+    MFHE_CHECK_LAUNCH("mfma_digitize_ifold_kernel");
+    for (int l0 = 0; l0 < L;) {
+        const int d = a.limbD ? std::max(a.limbD[l0], 5) : a.D;
+        int l1 = l0 + 1;
+        while (l1 < L && (a.limbD ? std::max(a.limbD[l1], 5) : a.D) == d) ++l1;
+        const dim3 grid(2 * Ppad / 64, FK / 64, l1 - l0);
+        if (a.pipe == 3) {
+            if (d == 5) hipLaunchKernelGGL((mod_gemm_mfma_ring_kernel<5, 2, true>), grid, dim3(256), 0, s, f, Ppad, l0);
+            else hipLaunchKernelGGL((mod_gemm_mfma_ring_kernel<6, 2, true>), grid, dim3(256), 0, s, f, Ppad, l0);
+        } else if (a.pipe != 1) {
+            if (d == 5) hipLaunchKernelGGL((mod_gemm_mfma_ring_kernel<5, 2, false>), grid, dim3(256), 0, s, f, Ppad, l0);
+            else hipLaunchKernelGGL((mod_gemm_mfma_ring_kernel<6, 2, false>), grid, dim3(256), 0, s, f, Ppad, l0);
+        } else {
+            if (d == 5) hipLaunchKernelGGL((mod_gemm_mfma_lds_kernel<5, 2>), grid, dim3(256), 0, s, f, Ppad, l0);
+            else hipLaunchKernelGGL((mod_gemm_mfma_lds_kernel<6, 2>), grid, dim3(256), 0, s, f, Ppad, l0);
+        }
+        MFHE_CHECK_LAUNCH("mod_gemm_mfma kernel (factored inverse)");
+        l0 = l1;
+    }
+    return MFHE_OK;
+}
+
 int launch_mod_gemm(const ModGemmArgs& a, int L, hipStream_t s) {
+    if (a.Adig && a.ifold) {
+        if (a.M != 512 || a.K != MK || !a.epi || a.D < 5 || a.D > 6 || !a.lds_stage || !a.iz || !a.phi)
+            return set_error(MFHE_EINVAL, "mod_gemm: factored inverse W-CRT needs M = K = 512, the FP64 epilogue and D in {5, 6}");
+        return launch_factored_inv(a, L, s);
+    }
     if (a.Adig && a.fold) {
         if (a.M != 512 || a.K != MK || !a.epi || a.D < 5 || a.D > 6 || !a.lds_stage)
             return set_error(MFHE_EINVAL, "mod_gemm: factored W-CRT needs M = K = 512, the FP64 epilogue and D in {5, 6}");
@@ -773,10 +1026,10 @@ int launch_mod_gemm(const ModGemmArgs& a, int L, hipStream_t s) {
 #define MFHE_MFMA_CASE(dd)                                                                                    \
     case dd:                                                                                                  \
         if (a.lds_stage && a.pipe == 3)                                                                       \
-            hipLaunchKernelGGL((mod_gemm_mfma_ring_kernel<dd, false, (dd <= 5)>), grid, dim3(256), 0, s, a, Ppad, l0); \
+            hipLaunchKernelGGL((mod_gemm_mfma_ring_kernel<dd, 0, (dd <= 5)>), grid, dim3(256), 0, s, a, Ppad, l0); \
         else if (a.lds_stage && a.pipe == 2)                                                                  \
-            hipLaunchKernelGGL((mod_gemm_mfma_ring_kernel<dd, false, false>), grid, dim3(256), 0, s, a, Ppad, l0); \
-        else if (a.lds_stage) hipLaunchKernelGGL((mod_gemm_mfma_lds_kernel<dd, false>), grid, dim3(256), 0, s, a, Ppad, l0); \
+            hipLaunchKernelGGL((mod_gemm_mfma_ring_kernel<dd, 0, false>), grid, dim3(256), 0, s, a, Ppad, l0); \
+        else if (a.lds_stage) hipLaunchKernelGGL((mod_gemm_mfma_lds_kernel<dd, 0>), grid, dim3(256), 0, s, a, Ppad, l0); \
         else hipLaunchKernelGGL(mod_gemm_mfma_kernel<dd>, grid, dim3(256), 0, s, a, Ppad, l0);                 \
         break;
                 MFHE_MFMA_CASE(5)

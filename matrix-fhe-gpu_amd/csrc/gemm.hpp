@@ -43,6 +43,12 @@ struct ModGemmArgs {
     // Z[i][k] = zeta^((i+1)(k+1)) and fold [L][16] its FP64 fold constants; null = dense GEMM
     const double* fold = nullptr;
     uint64_t* d0 = nullptr;      // set by the launcher (workspace after the digit planes)
+    // factored inverse W-CRT (gemm.hip): Adig holds the planes of Zi[i][k] = zeta^-((i+1)(k+1)), ifold [L][16]
+    // (q, 1/q, lam1[2][3], lam2[2][3]), iz [L][2][256] the dot-product rows, phi the packed Phi_771 rows; null = dense
+    const double* ifold = nullptr;
+    const double* iz = nullptr;
+    const uint8_t* phi = nullptr;
+    double* cc = nullptr;        // set by the launcher: [L][Ppad][2] (c0, c1) per column (the d0 workspace)
 };
 
 // bytes of B digit workspace the MFMA path needs for P columns and L limbs at D digits

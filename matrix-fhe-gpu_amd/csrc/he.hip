@@ -583,6 +583,14 @@ static int use_mfma(mfhe_ctx* c, ModGemmArgs& a, const uint64_t* A, int L) {
         a.adL = (uint64_t)c->wD * 256 * 256;
         a.fold = c->d_wfold;
     }
+    // ... and the inverse of a per-limb V^-1 (interpolation through 771 = 3 x 257, reduced mod Phi_771)
+    if (c->wcrt_mfma == 1 && A == c->d_wVinv && a.aL && c->d_wZidig && a.epi) {
+        a.Adig = c->d_wZidig;
+        a.adL = (uint64_t)c->wD * 256 * 256;
+        a.ifold = c->d_wifold;
+        a.iz = c->d_wiz;
+        a.phi = c->d_wphi;
+    }
     return MFHE_OK;
 }
 

@@ -98,6 +98,11 @@ struct mfhe_ctx {
     double* d_wepi = nullptr;    // [L][8] FP64 epilogue constants (gemm.hip GemmEpiF), null: integer epilogue
     int8_t* d_wZdig = nullptr;   // [L][wD][256][256] digits of Z[i][k] = zeta^((i+1)(k+1)) (factored forward W-CRT)
     double* d_wfold = nullptr;   // [L][16] factored forward fold constants (gemm.hip mfma_digitize_fold_kernel)
+    int8_t* d_wZidig = nullptr;  // [L][wD][256][256] digits of zeta^-((i+1)(k+1)) (factored inverse W-CRT)
+    double* d_wifold = nullptr;  // [L][16] factored inverse constants (q, 1/q, lam1[2][3], lam2[2][3])
+    double* d_wiz = nullptr;     // [L][2][256] zeta^(-255 (k+1)), zeta^(-256 (k+1)) (factored inverse dot products)
+    uint8_t* d_wphi = nullptr;   // [320] packed Phi_771 rows: byte r2 - 1 (r2 = 1..256; r2 = 0 at byte 256) holds
+                                 // phi_r2, phi_(r2-1), phi_(r2+257), phi_(r2+256) as (value + 1) at bits 0, 2, 4, 6
     int wcrt_mfma = 1;           // MFHE_OPT_WCRT_MFMA
     int wcrt_pipe = 0;           // MFHE_OPT_WCRT_PIPE
     int cgemm_mfma = 1;          // MFHE_OPT_CGEMM_MFMA

@@ -21,6 +21,10 @@
 
 namespace mfhe {
 
+#ifndef MFHE_NTT_CPOL_INV_COL_OUT
+#define MFHE_NTT_CPOL_INV_COL_OUT MFHE_NTT_CPOL_OUT   // the inverse's last (column) pass output stores
+#endif
+
 #ifndef MFHE_NTT_COLDB_NG
 #define MFHE_NTT_COLDB_NG 16   // columns per tile: 16 (128-B row segments, 2 workgroups/CU) or 32 (256 B, 1/CU)
 #endif
@@ -193,7 +197,7 @@ __device__ __forceinline__ void coldb_tile_inv(uint64_t* buf, uint32_t gl, uint3
     for (int k = 0; k < C::R; ++k)
         __builtin_amdgcn_raw_buffer_store_b64(
             __builtin_bit_cast(__attribute__((ext_vector_type(2))) unsigned, ar.canon(x[k])), rs,
-            (int)((off0 | ((uint32_t)Gm::g_of(0, tau, k) << logS)) * 8u), 0, MFHE_NTT_CPOL_OUT);
+            (int)((off0 | ((uint32_t)Gm::g_of(0, tau, k) << logS)) * 8u), 0, MFHE_NTT_CPOL_INV_COL_OUT);
 }
 
 // a limb's column-pass twiddles into registers (tw0 shared, tw1 per thread), see coldb_tile.  tw0 is the same

@@ -54,3 +54,20 @@ c1q=h[513]; c0q=(h[512]-c1q*phi[511])%q
 f=[(h[r]-c0q*phi[r]-(c1q*phi[r-1] if r>0 else 0))%q for r in range(512)]
 chk=[sum(pow(eta,e*r,q)*f[r] for r in range(512))%q for e in exp]
 print("inverse: V f == y:", chk == y, " f == x:", f == x)
+# the factored inverse as gemm.hip computes it: E_a[r2] (r2 = 1..256) from the 256 x 256 GEMM with
+# Zi[i][k] = zeta^-((i+1)(k+1)); E_a[0], E_a[255], E_a[256] also by dot products in the digitize kernel;
+# h_r2 = sum_a lam1[a][r2 % 3] E_a[r2], h_(r2+257) = sum_a lam2[a][r2 % 3] E_a[r2]; f_j = h_j - c0 phi_j - c1 phi_(j-1)
+kap=[[inv771*pow(om,(-(ap+1)*t)%3,q)%q for t in range(3)] for ap in range(2)]
+lam1=[[(kap[ap][t]-kap[ap][(t+1)%3])%q for t in range(3)] for ap in range(2)]
+lam2=[[(kap[ap][(t+2)%3]-kap[ap][(t+1)%3])%q for t in range(3)] for ap in range(2)]
+zi=pow(ze,256,q)
+EE=[[sum(pow(zi,(r2*(b+1))%257,q)*y[ap*256+b] for b in range(256))%q for r2 in range(257)] for ap in range(2)]
+hh=[0]*514
+for r2 in range(257):
+    t=r2%3
+    hh[r2]=sum(lam1[ap][t]*EE[ap][r2] for ap in range(2))%q
+    hh[r2+257]=sum(lam2[ap][t]*EE[ap][r2] for ap in range(2))%q
+print("inverse h via lambda == h:", hh == h)
+cc1=hh[513]; cc0=(hh[512]-cc1*phi[511])%q
+ff=[(hh[j]-cc0*phi[j]-(cc1*phi[j-1] if j>0 else 0))%q for j in range(512)]
+print("inverse via lambda: f == x:", ff == x)
