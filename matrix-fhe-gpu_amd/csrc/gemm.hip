@@ -601,11 +601,18 @@ __device__ __forceinline__ void mfma_epilogue(const ModGemmArgs& a, const v16i (
         const int ap = colf & 1;
         const uint32_t p = colf >> 1;
         const bool live = p < a.P;   // the same for both lanes of a pair
-        double lam1[3], lam2[3];
+        // this lane's output takes lam_own (lam1 for a' = 0, lam2 for a' = 1) of its own E and the partner's share
+        // lam_oth; both rotated once by r2 mod 3 of the lane's first row, so row reg uses index (reg's offset) mod 3
+        const int r2b = m0 + 4 * h + 1;   // r2 of reg 0; reg adds (reg & 3) + 8 (reg >> 2)
+        const int tb = r2b % 3;
+        double own[3], oth[3];
 #pragma unroll
-        for (int t = 0; t < 3; ++t) {
-            lam1[t] = ap ? fo[5 + t] : fo[2 + t];
-            lam2[t] = ap ? fo[11 + t] : fo[8 + t];
+        for (int k = 0; k < 3; ++k) {
+            const int t = tb + k >= 3 ? tb + k - 3 : tb + k;
+            const double l1 = t == 0 ? (ap ? fo[5] : fo[2]) : (t == 1 ? (ap ? fo[6] : fo[3]) : (ap ? fo[7] : fo[4]));
+            const double l2 = t == 0 ? (ap ? fo[11] : fo[8]) : (t == 1 ? (ap ? fo[12] : fo[9]) : (ap ? fo[13] : fo[10]));
+            own[k] = ap ? l2 : l1;
+            oth[k] = ap ? l1 : l2;
         }
         const double c0 = cc.c0, c1 = cc.c1;
         uint64_t* Cp = Cl + (uint64_t)(p >> a.log_n) * a.scY + (p & ((1u << a.log_n) - 1));
@@ -617,9 +624,12 @@ __device__ __forceinline__ void mfma_epilogue(const ModGemmArgs& a, const v16i (
         for (int i = 0; i < 8; ++i) win[i] = pw[i];
         const int sh = ap ? 4 : 0;   // fields (phi_j, phi_(j-1)) of this lane's output row j
         constexpr int NZ = (NS + 1) / 2, NY = (NZ + 1) / 2;
+        // every row computed first, the guarded stores after: a store under a branch inside the row loop splits it
+        // into 16 serial blocks, each paying the full FP64 latency chain
+        uint64_t outw[16];
 #pragma unroll
         for (int reg = 0; reg < 16; ++reg) {
-            const int r2 = m0 + (reg & 3) + 8 * (reg >> 2) + 4 * h + 1;
+            const int k = ((reg & 3) + 8 * (reg >> 2)) % 3;
             const uint32_t pb = ((h ? win[2 * (reg >> 2) + 1] : win[2 * (reg >> 2)]) >> (8 * (reg & 3) + sh)) & 15u;
             double zz[NZ];
 #pragma unroll
@@ -632,17 +642,16 @@ __device__ __forceinline__ void mfma_epilogue(const ModGemmArgs& a, const v16i (
                 const double y = 2 * u + 1 < NZ ? __fma_rn(65536.0, zz[2 * u + 1], zz[2 * u]) : zz[2 * u];
                 v += u == 0 ? y : ar.mulmod(y, c32[u - 1]);
             }
-            const double e = ar.reduce(v);
-            const uint32_t t = (uint32_t)r2 % 3u;
-            const double w1 = t == 0 ? lam1[0] : (t == 1 ? lam1[1] : lam1[2]);
-            const double w2 = t == 0 ? lam2[0] : (t == 1 ? lam2[1] : lam2[2]);
-            const double p1 = ar.mulmod(e, w1), p2 = ar.mulmod(e, w2);
-            const double got = swap_pair(ap ? p1 : p2);   // the partner's share of this lane's output
-            const double hv = (ap ? p2 : p1) + got;
-            const int j = ap ? r2 + 257 : r2;
-            if (live && (ap == 0 || r2 <= 254)) {
-                const double fj = hv - c0 * (double)((int)(pb & 3u) - 1) - c1 * (double)((int)(pb >> 2) - 1);
-                Cp[(uint64_t)j * a.scM] = ar.canon(fj);
+            // |v| < 2^51 + 2 q, so v * lam / q < 2^51 with |lam| <= q / 2: mulmod needs no reduction of v first
+            const double hv = ar.mulmod(v, own[k]) + swap_pair(ar.mulmod(v, oth[k]));
+            const double fj = hv - c0 * (double)((int)(pb & 3u) - 1) - c1 * (double)((int)(pb >> 2) - 1);
+            outw[reg] = ar.canon(fj);
+        }
+        if (live) {
+#pragma unroll
+            for (int reg = 0; reg < 16; ++reg) {
+                const int r2 = r2b + (reg & 3) + 8 * (reg >> 2);
+                if (ap == 0 || r2 <= 254) Cp[(uint64_t)(ap ? r2 + 257 : r2) * a.scM] = outw[reg];
             }
         }
         return;

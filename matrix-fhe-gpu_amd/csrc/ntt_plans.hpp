@@ -36,6 +36,9 @@
 #ifndef MFHE_NTT_NGB17
 #define MFHE_NTT_NGB17 4    // N = 2^17 forward: 512-element rows per block-pass workgroup (8 -> 4: +0.9% C5 shard)
 #endif
+#ifndef MFHE_NTT_INV16_PLAIN_NG
+#define MFHE_NTT_INV16_PLAIN_NG 0   // N = 2^16 inverse last pass: 0 = DMA column pass; 16 / 32 = plain column pass (A/B)
+#endif
 
 namespace mfhe {
 
@@ -342,6 +345,8 @@ static int run_phantom(const NttJob<TS>& j, hipStream_t st) {
         case 16:
             // the packed intermediate's units are laid out for 16-row block tiles
             if (!INV && j.pack) return two_pass<A, TS, 8, 16, 8, 16, INV>(j, st);
+            if constexpr (INV && MFHE_NTT_INV16_PLAIN_NG > 0)
+                return two_pass<A, TS, 8, MFHE_NTT_INV16_PLAIN_NG, 8, MFHE_NTT_NGB16, INV>(j, st);
             return two_pass<A, TS, 8, 16, 8, MFHE_NTT_NGB16, INV>(j, st);
         // N = 2^17: the forward column pass takes 8 stages on 16-column tiles (128-B row segments) and the block
         // pass 9; the inverse keeps 9 column + 8 block stages.  Measured per direction (profiles/r02_n17_split.txt):
