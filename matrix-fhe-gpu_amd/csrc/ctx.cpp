@@ -336,7 +336,7 @@ static int build_wcrt(mfhe_ctx* c) {
                 // zeta^-((i+1)(k+1)); kappa[a][t] = 771^-1 omega^(-a t); lam1[a][t] = kappa[a][t] - kappa[a][t+1],
                 // lam2[a][t] = kappa[a][t+2] - kappa[a][t+1] (t mod 3); z[l][0 / 1][k] = zeta^(-255 / -256 (k+1)).
                 std::vector<int8_t> zid((size_t)L * D * FK * FK);
-                std::vector<double> ifo((size_t)L * 16, 0.0), iz((size_t)L * 2 * FK);
+                std::vector<double> ifo((size_t)L * 16, 0.0), iz((size_t)L * 48, 0.0);
                 for (int l = 0; l < L; ++l) {
                     const uint64_t q = c->moduli[l], eta = hm::find_eta771(q);
                     const uint64_t zinv = hm::powmod(hm::powmod(eta, 3, q), 256, q), omega = hm::powmod(eta, 257, q);
@@ -363,11 +363,11 @@ static int build_wcrt(mfhe_ctx* c) {
                             ifo[(size_t)l * 16 + 2 + 3 * ap + t] = centred(sub(kap[ap][t], kap[ap][(t + 1) % 3]), q);
                             ifo[(size_t)l * 16 + 8 + 3 * ap + t] = centred(sub(kap[ap][(t + 2) % 3], kap[ap][(t + 1) % 3]), q);
                         }
-                    for (int s = 0; s < 2; ++s) {
-                        const uint64_t zs = hm::powmod(zinv, 255 + (uint64_t)s, q);
-                        uint64_t cur = zs;
-                        for (int k = 0; k < FK; ++k, cur = hm::mulmod(cur, zs, q))
-                            iz[((size_t)l * 2 + s) * FK + k] = centred(cur, q);
+                    for (int s = 0; s < 2; ++s) {   // x_s = zeta^-(255 + s): x_s, then x_s^(16 j + 1), j < 16
+                        const uint64_t xs = hm::powmod(zinv, 255 + (uint64_t)s, q);
+                        iz[(size_t)l * 48 + s] = centred(xs, q);
+                        for (int j = 0; j < 16; ++j)
+                            iz[(size_t)l * 48 + 16 + 16 * s + j] = centred(hm::powmod(xs, 16 * (uint64_t)j + 1, q), q);
                     }
                 }
                 // Phi_771 = (x^514 + x^257 + 1) / (x^2 + x + 1), coefficients in {-1, 0, 1}; phi[j + 1] = coefficient j

@@ -447,7 +447,6 @@ __global__ __launch_bounds__(256) void mfma_digitize_fold_kernel(const uint64_t*
 template <int D>
 __global__ __launch_bounds__(256) void mfma_digitize_ifold_kernel(ModGemmArgs a, uint32_t Ppad, PlaneCounts pc) {
     __shared__ double red[3][4][64];
-    __shared__ double z[2 * FK];   // the limb's dot-product rows zeta^(-255 b), zeta^(-256 b)
     const int lane = threadIdx.x & 63, kq = threadIdx.x >> 6;
     const uint32_t p = blockIdx.x * 16 + (lane >> 2);
     const int ap = (lane >> 1) & 1, hf = lane & 1;
@@ -458,9 +457,10 @@ __global__ __launch_bounds__(256) void mfma_digitize_ifold_kernel(ModGemmArgs a,
     lc.qf = fo[0];
     lc.qinv = fo[1];
     const ArithF64 ar(lc);
-    z[threadIdx.x] = a.iz[(uint64_t)l * 2 * FK + threadIdx.x];
-    z[threadIdx.x + 256] = a.iz[(uint64_t)l * 2 * FK + 256 + threadIdx.x];
-    __syncthreads();
+    // iz[l] = (x1, x2, pad[14], x1^(16 j + 1) for j < 16, x2^(16 j + 1) for j < 16), x1 = zeta^-255, x2 = zeta^-256
+    const double* izl = a.iz + (uint64_t)l * 48;
+    const double x1 = ((cdp_t)izl)[0], x2 = ((cdp_t)izl)[1];
+    const double* zp = izl + 16;
     const uint64_t* Bl = a.B + (uint64_t)l * a.bL;
     const uint32_t nmask = (1u << a.log_n) - 1;
     const uint64_t col = (uint64_t)(p >> a.log_n) * a.sbY + (p & nmask);
@@ -482,20 +482,21 @@ __global__ __launch_bounds__(256) void mfma_digitize_ifold_kernel(ModGemmArgs a,
             v[kk] = ArithF64::from_u64(Bl[(uint64_t)(ap * FK + k0 + kk) * a.sbK + cl]);
 #pragma unroll
         for (int kk = 0; kk < 16; ++kk) v[kk] = live ? ar.reduce(v[kk]) : 0.0;
-        // the three dot products as two independent chains each (exact: |partial| < 9 q < 2^54 is never reached,
-        // every chain is re-centred after 4 terms)
-        double t0[2] = {0.0, 0.0}, t1[2] = {0.0, 0.0}, t2[2] = {0.0, 0.0};
+        // sum_b x^b v_b over this chunk (b = k0 + 1 + i) as x^(k0+1) * Horner(v, x) for x = zeta^-255, zeta^-256:
+        // no per-element table, two independent chains (|h| <= q + 1 between steps: mulmod's range holds)
+        double h1 = v[15], h2 = v[15], t0 = 0.0;
+#pragma unroll
+        for (int kk = 14; kk >= 0; --kk) {
+            h1 = ar.mulmod(h1, x1) + v[kk];
+            h2 = ar.mulmod(h2, x2) + v[kk];
+        }
+#pragma unroll
+        for (int kk = 0; kk < 16; ++kk) t0 += v[kk];   // |t0| <= 8 q < 2^53
+        s0 = ar.reduce(s0 + t0);
+        s1 = ar.reduce(s1 + ar.mulmod(h1, zp[(k0 >> 4)]));
+        s2 = ar.reduce(s2 + ar.mulmod(h2, zp[16 + (k0 >> 4)]));
 #pragma unroll
         for (int kk = 0; kk < 16; ++kk) {
-            const int c = kk & 1;
-            t0[c] += v[kk];
-            t1[c] += ar.mulmod(v[kk], z[k0 + kk]);
-            t2[c] += ar.mulmod(v[kk], z[FK + k0 + kk]);
-            if ((kk & 7) >= 6) {
-                t0[c] = ar.reduce(t0[c]);
-                t1[c] = ar.reduce(t1[c]);
-                t2[c] = ar.reduce(t2[c]);
-            }
             const uint64_t y = balanced_bytes<D>(v[kk]);
             const uint32_t lo = (uint32_t)y, hi = (uint32_t)(y >> 32);
 #pragma unroll
@@ -504,9 +505,6 @@ __global__ __launch_bounds__(256) void mfma_digitize_ifold_kernel(ModGemmArgs a,
                 pk[i][kk >> 2] |= b << (8 * (kk & 3));
             }
         }
-        s0 = ar.reduce(s0 + t0[0] + t0[1]);
-        s1 = ar.reduce(s1 + t1[0] + t1[1]);
-        s2 = ar.reduce(s2 + t2[0] + t2[1]);
 #pragma unroll
         for (int i = 0; i < D; ++i) {
             if (i >= nd) break;

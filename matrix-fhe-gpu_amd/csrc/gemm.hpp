@@ -44,7 +44,8 @@ struct ModGemmArgs {
     const double* fold = nullptr;
     uint64_t* d0 = nullptr;      // set by the launcher (workspace after the digit planes)
     // factored inverse W-CRT (gemm.hip): Adig holds the planes of Zi[i][k] = zeta^-((i+1)(k+1)), ifold [L][16]
-    // (q, 1/q, lam1[2][3], lam2[2][3]), iz [L][2][256] the dot-product rows, phi the packed Phi_771 rows; null = dense
+    // (q, 1/q, lam1[2][3], lam2[2][3]), iz [L][48] the dot-product points and chunk powers, phi the packed Phi_771
+    // rows; null = dense
     const double* ifold = nullptr;
     const double* iz = nullptr;
     const uint8_t* phi = nullptr;

@@ -304,6 +304,12 @@ __global__ __launch_bounds__(256) void enc_ring_kernel(RingArgs ra, const uint64
     uint64_t av[4], sk[4];
     ld4(aev + p0, av);
     ld4(ra.sk + ((uint64_t)w * ra.L + l) * N + 4 * j, sk);
+    // the combine's operands are loaded before the ring product (clamped rows for dead lanes), so their latency
+    // overlaps the butterflies instead of following them
+    uint64_t ev[4], mv[4], mi[4], b[4];
+    ld4(e + p0, ev);
+    ld4(m_re + i0, mv);
+    if (m_im) ld4(m_im + i0, mi);
     double x[4], sv[4];
 #pragma unroll
     for (int s = 0; s < 4; ++s) {
@@ -313,23 +319,19 @@ __global__ __launch_bounds__(256) void enc_ring_kernel(RingArgs ra, const uint64
     ring_mul_row<LOGN>(x, sv, j, ar, ra.tw + l * N, ra.itw + l * N, ra.ninv[l]);
     if (!live) return;
     const uint64_t q = lc.q, total = ra.rows * N;
-    uint64_t ev[4], mv[4], b[4];
-    ld4(e + p0, ev);
     auto bval = [&](uint64_t m, int s) {
         const uint64_t tv = ar.canon(x[s]);
         uint64_t d = m >= tv ? m - tv : m + q - tv;
         d += ev[s];
         return d >= q ? d - q : d;
     };
-    ld4(m_re + i0, mv);
 #pragma unroll
     for (int s = 0; s < 4; ++s) b[s] = bval(mv[s], s);
     st4(ct_re + i0, b);
     st4(ct_re + total + i0, av);
     if (m_im) {
-        ld4(m_im + i0, mv);
 #pragma unroll
-        for (int s = 0; s < 4; ++s) b[s] = bval(mv[s], s);
+        for (int s = 0; s < 4; ++s) b[s] = bval(mi[s], s);
         st4(ct_im + i0, b);
         st4(ct_im + total + i0, av);
     }
@@ -352,9 +354,10 @@ __global__ __launch_bounds__(256) void dec_ring_kernel(RingArgs ra, const uint64
     const uint64_t p0 = (((uint64_t)w * N + y) * ra.L + l) * N + 4 * j;
     const LimbConst lc = ra.lf[l];
     const ArithF64 ar(lc);
-    uint64_t av[4], sk[4];
+    uint64_t av[4], sk[4], bv[4];
     ld4(ct + total + i0, av);
     ld4(ra.sk + ((uint64_t)w * ra.L + l) * N + 4 * j, sk);
+    ld4(ct + i0, bv);   // before the ring product, so its latency overlaps the butterflies (clamped row if dead)
     double x[4], sv[4];
 #pragma unroll
     for (int s = 0; s < 4; ++s) {
@@ -363,8 +366,6 @@ __global__ __launch_bounds__(256) void dec_ring_kernel(RingArgs ra, const uint64
     }
     ring_mul_row<LOGN>(x, sv, j, ar, ra.tw + l * N, ra.itw + l * N, ra.ninv[l]);
     if (!live) return;
-    uint64_t bv[4];
-    ld4(ct + i0, bv);
 #pragma unroll
     for (int s = 0; s < 4; ++s) {
         const uint64_t sum = bv[s] + ar.canon(x[s]);

@@ -100,7 +100,7 @@ struct mfhe_ctx {
     double* d_wfold = nullptr;   // [L][16] factored forward fold constants (gemm.hip mfma_digitize_fold_kernel)
     int8_t* d_wZidig = nullptr;  // [L][wD][256][256] digits of zeta^-((i+1)(k+1)) (factored inverse W-CRT)
     double* d_wifold = nullptr;  // [L][16] factored inverse constants (q, 1/q, lam1[2][3], lam2[2][3])
-    double* d_wiz = nullptr;     // [L][2][256] zeta^(-255 (k+1)), zeta^(-256 (k+1)) (factored inverse dot products)
+    double* d_wiz = nullptr;     // [L][48] x1, x2 (zeta^-255, zeta^-256), pad, x1^(16j+1), x2^(16j+1) for j < 16
     uint8_t* d_wphi = nullptr;   // [320] packed Phi_771 rows: byte r2 - 1 (r2 = 1..256; r2 = 0 at byte 256) holds
                                  // phi_r2, phi_(r2-1), phi_(r2+257), phi_(r2+256) as (value + 1) at bits 0, 2, 4, 6
     int wcrt_mfma = 1;           // MFHE_OPT_WCRT_MFMA
