@@ -642,14 +642,21 @@ __device__ __forceinline__ void mfma_epilogue(const ModGemmArgs& a, const v16i (
             }
             // |v| < 2^51 + 2 q, so v * lam / q < 2^51 with |lam| <= q / 2: mulmod needs no reduction of v first
             const double hv = ar.mulmod(v, own[k]) + swap_pair(ar.mulmod(v, oth[k]));
-            const double fj = hv - c0 * (double)((int)(pb & 3u) - 1) - c1 * (double)((int)(pb >> 2) - 1);
+            // phi in {-1, 0, 1}: exact products, so one fma each
+            const double fj = __fma_rn(-c0, (double)((int)(pb & 3u) - 1), __fma_rn(-c1, (double)((int)(pb >> 2) - 1), hv));
             outw[reg] = ar.canon(fj);
         }
         if (live) {
+            const uint64_t jb = (uint64_t)(ap ? r2b + 257 : r2b);
+            if (m0 + 32 <= 254) {   // wave-uniform: every row of this tile has an output in both halves
 #pragma unroll
-            for (int reg = 0; reg < 16; ++reg) {
-                const int r2 = r2b + (reg & 3) + 8 * (reg >> 2);
-                if (ap == 0 || r2 <= 254) Cp[(uint64_t)(ap ? r2 + 257 : r2) * a.scM] = outw[reg];
+                for (int reg = 0; reg < 16; ++reg) Cp[(jb + (reg & 3) + 8 * (reg >> 2)) * a.scM] = outw[reg];
+            } else {
+#pragma unroll
+                for (int reg = 0; reg < 16; ++reg) {
+                    const int r2 = r2b + (reg & 3) + 8 * (reg >> 2);
+                    if (ap == 0 || r2 <= 254) Cp[(jb + (reg & 3) + 8 * (reg >> 2)) * a.scM] = outw[reg];
+                }
             }
         }
         return;
