@@ -252,6 +252,50 @@ static int build_wcrt(mfhe_ctx* c) {
     if ((rc = upload(c, &c->d_wV, V)) || (rc = upload(c, &c->d_wVinv, Vi)) || (rc = upload(c, &c->d_wdV, wdv)) ||
         (rc = upload(c, &c->d_wdVinv, wdvi)))
         return rc;
+    {
+        // factored W-DFT tables (the complex counterpart of the factored W-CRT below; tools/wcrt_factor_check.py):
+        // entries from exact integer exponents, so each is cos / sin of one angle (no repeated-product drift)
+        auto cis = [](long num, long den) {
+            const double two_pi = 6.283185307179586476925286766559;
+            const long e = ((num % den) + den) % den;
+            return make_double2(std::cos(two_pi * (double)e / (double)den), std::sin(two_pi * (double)e / (double)den));
+        };
+        std::vector<double2> zc(256 * 256), zic(256 * 256), lam(12), xp(512);
+        for (int i = 0; i < 256; ++i)
+            for (int k = 0; k < 256; ++k) {
+                const long e = ((long)(i + 1) * (k + 1)) % 257;
+                zc[(size_t)i * 256 + k] = cis(e, 257);
+                zic[(size_t)i * 256 + k] = cis(-e, 257);
+            }
+        double2 kap[2][3];
+        for (int ap = 0; ap < 2; ++ap)
+            for (int t = 0; t < 3; ++t) {
+                const double2 w = cis(-(long)((ap + 1) * t), 3);
+                kap[ap][t] = make_double2(w.x / 771.0, w.y / 771.0);
+            }
+        auto sub = [](double2 x, double2 y) { return make_double2(x.x - y.x, x.y - y.y); };
+        for (int ap = 0; ap < 2; ++ap)
+            for (int t = 0; t < 3; ++t) {
+                lam[(0 * 2 + ap) * 3 + t] = sub(kap[ap][t], kap[ap][(t + 1) % 3]);
+                lam[(1 * 2 + ap) * 3 + t] = sub(kap[ap][(t + 2) % 3], kap[ap][(t + 1) % 3]);
+            }
+        for (int s = 0; s < 2; ++s)
+            for (int k = 0; k < 256; ++k) xp[(size_t)s * 256 + k] = cis(-(long)(255 + s) * (k + 1), 257);
+        std::vector<int> num(515, 0), ph(513, 0);   // Phi_771 = (x^514 + x^257 + 1) / (x^2 + x + 1)
+        num[0] = num[257] = num[514] = 1;
+        for (int d = 514; d >= 2; --d)
+            if (num[d]) {
+                const int cf = num[d];
+                ph[d - 2] = cf;
+                num[d] -= cf;
+                num[d - 1] -= cf;
+                num[d - 2] -= cf;
+            }
+        std::vector<int8_t> phi(ph.begin(), ph.end());
+        if ((rc = upload(c, &c->d_wdZ, zc)) || (rc = upload(c, &c->d_wdZi, zic)) || (rc = upload(c, &c->d_wdlam, lam)) ||
+            (rc = upload(c, &c->d_wdxp, xp)) || (rc = upload(c, &c->d_wdphi, phi)))
+            return rc;
+    }
     // i8 MFMA operand planes (gemm.hip): D balanced base-256 digits of every V / V^-1 entry, and
     // 256^s mod q for the epilogue.  Needs 2^27 < q (|acc_s| < q) and q < 2^59 (D <= 8).
     bool big = true;
@@ -564,6 +608,7 @@ extern "C" int mfhe_ctx_destroy(mfhe_ctx* c) {
     if (c->ws) (void)hipFree(c->ws);
     if (c->fused_buf) (void)hipFree(c->fused_buf);
     if (c->gemm_ws) (void)hipFree(c->gemm_ws);
+    if (c->wd_ws) (void)hipFree(c->wd_ws);
     for (void* p : c->allocs) (void)hipFree(p);
     delete c;
     return MFHE_OK;
@@ -647,7 +692,7 @@ extern "C" int mfhe_ctx_set_option(mfhe_ctx* c, int opt, int64_t v) {
             c->wcrt_pipe = (int)v;
             return MFHE_OK;
         case MFHE_OPT_CGEMM_MFMA:
-            if (v < 0 || v > 1) return set_error(MFHE_EINVAL, "cgemm mfma must be 0 or 1");
+            if (v < 0 || v > 2) return set_error(MFHE_EINVAL, "cgemm mfma must be 0, 1 or 2");
             c->cgemm_mfma = (int)v;
             return MFHE_OK;
         case MFHE_OPT_HE_FUSED:

@@ -163,6 +163,23 @@ typedef double v4d __attribute__((ext_vector_type(4)));
 constexpr int CKT = 16;          // K per LDS stage
 constexpr int CAP = CKT + 1;     // A plane row pitch (doubles): spreads a fragment's 16 rows over the banks
 
+// omega^e, omega = e^(2 pi i / 3) (the order-3 root of the factored W-DFT)
+__device__ __forceinline__ double2 omega3(int e) {
+    constexpr double h = 0.86602540378443864676;   // sqrt(3) / 2
+    return e == 0 ? make_double2(1.0, 0.0) : make_double2(-0.5, e == 1 ? h : -h);
+}
+__device__ __forceinline__ double2 cmul(double2 x, double2 y) {
+    return make_double2(__fma_rn(x.x, y.x, -x.y * y.y), __fma_rn(x.x, y.y, x.y * y.x));
+}
+// lanes l <-> l ^ 1 (DPP quad_perm [1, 0, 3, 2])
+__device__ __forceinline__ double dpp_swap1(double x) {
+    const int lo = __double2loint(x), hi = __double2hiint(x);
+    return __hiloint2double(__builtin_amdgcn_mov_dpp(hi, 0xB1, 0xF, 0xF, true),
+                            __builtin_amdgcn_mov_dpp(lo, 0xB1, 0xF, 0xF, true));
+}
+
+// FAC (a.fac): 0 dense; 1 / 2 the factored forward / inverse W-DFT (gemm.hpp CGemmArgs::fac)
+template <int FAC>
 __global__ __launch_bounds__(NTH, 2) void cgemm_mfma_kernel(CGemmArgs a) {
     __shared__ double Ar[2][TM * CAP], Ai[2][TM * CAP];   // [row][k]
     __shared__ double Br[2][CKT * TP], Bi[2][CKT * TP];   // [k][col]
@@ -184,7 +201,25 @@ __global__ __launch_bounds__(NTH, 2) void cgemm_mfma_kernel(CGemmArgs a) {
         for (int e = 0; e < (CKT * TP) / NTH; ++e) {   // B stage 16 x 64, coalesced along p
             const int idx = t + e * NTH, k = k0 + (idx >> 6);
             const uint32_t p = p0 + (idx & 63);
-            rb[e] = (k < a.K && p < a.P) ? B[b_off(k, p, a.sbK, a.sbY, a.log_n)] : make_double2(0, 0);
+            if constexpr (FAC == 0) {
+                rb[e] = (k < a.K && p < a.P) ? B[b_off(k, p, a.sbK, a.sbY, a.log_n)] : make_double2(0, 0);
+            } else if constexpr (FAC == 1) {
+                // F_a[r2] = omega^(a t) in[r2] + omega^(a ((t + 2) mod 3)) in[r2 + 257], r2 = k + 1, t = r2 mod 3
+                const bool live = p < a.P;
+                const int ap = p >= a.Pf;
+                const uint32_t pc = live ? p - ap * a.Pf : 0;
+                const int r2 = k + 1, t3 = r2 % 3, r3 = r2 + 257 < 512 ? r2 + 257 : 511;
+                const double2 x1 = B[(uint64_t)r2 * a.Pf + pc], x2 = B[(uint64_t)r3 * a.Pf + pc];
+                const double2 f1 = cmul(omega3(((ap + 1) * t3) % 3), x1);
+                const double2 f2 = r2 + 257 < 512 ? cmul(omega3(((ap + 1) * ((t3 + 2) % 3)) % 3), x2) : make_double2(0, 0);
+                rb[e] = live ? make_double2(f1.x + f2.x, f1.y + f2.y) : make_double2(0, 0);
+            } else {
+                // y[a'][b] = in[a' 256 + k][p] in interleaved columns 2 p + a'
+                const bool live = p < a.P;
+                const uint32_t pc = live ? p >> 1 : 0;
+                const double2 y = B[(uint64_t)((p & 1) * 256 + k) * a.Pf + pc];
+                rb[e] = live ? y : make_double2(0, 0);
+            }
         }
     };
     auto store = [&](int buf) {
@@ -248,6 +283,55 @@ __global__ __launch_bounds__(NTH, 2) void cgemm_mfma_kernel(CGemmArgs a) {
         __syncthreads();
     }
     double2* C = a.C + (uint64_t)bt * a.cB;
+    if constexpr (FAC == 1) {
+        // out[a' 256 + m][p] = GEMM + F_a[0], F_a[0] = in[0] + omega^(2 a) in[257]
+#pragma unroll
+        for (int j = 0; j < 2; ++j) {
+            const uint32_t c = p0 + wp + 16 * j + r;
+            if (c >= a.P) continue;
+            const int ap = c >= a.Pf;
+            const uint32_t p = c - ap * a.Pf;
+            const double2 f = cmul(omega3((2 * (ap + 1)) % 3), B[257ull * a.Pf + p]), x0 = B[p];
+            const double2 add = make_double2(x0.x + f.x, x0.y + f.y);
+#pragma unroll
+            for (int i = 0; i < 2; ++i)
+#pragma unroll
+                for (int g = 0; g < 4; ++g) {
+                    const int m = m0 + wm + 16 * i + kq + 4 * g;
+                    C[(uint64_t)(ap * 256 + m) * a.scM + p] = make_double2(cr[i][j][g] + add.x, ci[i][j][g] + add.y);
+                }
+        }
+        return;
+    } else if constexpr (FAC == 2) {
+        // E_a'[r2] (r2 = m + 1) in lanes 2p + a'; h_r2 = sum_a lam1[a][t] E_a, h_(r2+257) = sum_a lam2[a][t] E_a
+        // (t = r2 mod 3), f_j = h_j - c0 phi_j - c1 phi_(j-1): lane a' = 0 writes row r2, a' = 1 row r2 + 257
+#pragma unroll
+        for (int j = 0; j < 2; ++j) {
+            const uint32_t c = p0 + wp + 16 * j + r;
+            const int ap = c & 1;
+            const uint32_t p = c >> 1;
+            const bool live = c < a.P;   // the same for both lanes of a pair (P even)
+            const uint32_t pc = live ? p : 0;
+            const double2 c0 = a.cc[2ull * pc], c1 = a.cc[2ull * pc + 1];
+#pragma unroll
+            for (int i = 0; i < 2; ++i)
+#pragma unroll
+                for (int g = 0; g < 4; ++g) {
+                    const int r2 = m0 + wm + 16 * i + kq + 4 * g + 1;
+                    const int t3 = r2 % 3;
+                    const double2 own = a.lam[(ap * 2 + ap) * 3 + t3], oth = a.lam[((1 - ap) * 2 + ap) * 3 + t3];
+                    const double2 e = make_double2(cr[i][j][g], ci[i][j][g]);
+                    const double2 po = cmul(own, e), ps = cmul(oth, e);
+                    const double hx = po.x + dpp_swap1(ps.x), hy = po.y + dpp_swap1(ps.y);
+                    const int jr = ap ? r2 + 257 : r2;
+                    if (live && jr < 512) {
+                        const double f0 = (double)a.phi[jr], f1 = (double)a.phi[jr - 1];
+                        C[(uint64_t)jr * a.scM + p] = make_double2(hx - c0.x * f0 - c1.x * f1, hy - c0.y * f0 - c1.y * f1);
+                    }
+                }
+        }
+        return;
+    }
 #pragma unroll
     for (int i = 0; i < 2; ++i)
 #pragma unroll
@@ -260,6 +344,74 @@ __global__ __launch_bounds__(NTH, 2) void cgemm_mfma_kernel(CGemmArgs a) {
                 if (m < a.M) C[b_off(m, p, a.scM, a.scY, a.log_n)] = make_double2(cr[i][j][g], ci[i][j][g]);
             }
         }
+}
+
+// factored inverse W-DFT, rows r2 = 0, 255, 256 of E_a by dot products.  One thread per (column p, a', 32-row
+// chunk q): lane = 2 p_local + a' (16 columns per block), q = thread / 32.  S0 = sum y, S1 = sum x1^b y,
+// S2 = sum x2^b y over b = 32 q + 1 .. 32 q + 32; the chunks reduce through LDS, a' by a lane exchange; then
+// f_0, f_257 and (c0, c1) as in mfma_digitize_ifold_kernel (complex, no reduction mod q).
+__global__ __launch_bounds__(256) void cwdft_inv_dots_kernel(CGemmArgs a, const double2* __restrict__ in,
+                                                             const double2* __restrict__ xpow) {
+    __shared__ double2 red[3][8][32];
+    const int lane = threadIdx.x & 31, q = threadIdx.x >> 5;   // 32 threads = 16 columns x 2 a'; 8 chunks
+    const uint32_t p = blockIdx.x * 16 + (lane >> 1);
+    const int ap = lane & 1;
+    const bool live = p < a.Pf;
+    const uint32_t pc = live ? p : 0;
+    double2 s0 = make_double2(0, 0), s1 = s0, s2 = s0;
+#pragma unroll 8
+    for (int i = 0; i < 32; ++i) {
+        const int k = q * 32 + i;   // b = k + 1
+        const double2 y = in[(uint64_t)(ap * 256 + k) * a.Pf + pc];
+        const double2 z1 = xpow[k], z2 = xpow[256 + k];
+        s0.x += y.x;
+        s0.y += y.y;
+        s1.x = __fma_rn(z1.x, y.x, __fma_rn(-z1.y, y.y, s1.x));
+        s1.y = __fma_rn(z1.x, y.y, __fma_rn(z1.y, y.x, s1.y));
+        s2.x = __fma_rn(z2.x, y.x, __fma_rn(-z2.y, y.y, s2.x));
+        s2.y = __fma_rn(z2.x, y.y, __fma_rn(z2.y, y.x, s2.y));
+    }
+    red[0][q][lane] = s0;
+    red[1][q][lane] = s1;
+    red[2][q][lane] = s2;
+    __syncthreads();
+    if (q != 0) return;
+    double2 e[3];
+#pragma unroll
+    for (int v = 0; v < 3; ++v) {
+        double2 acc = red[v][0][lane];
+#pragma unroll
+        for (int c = 1; c < 8; ++c) acc = make_double2(acc.x + red[v][c][lane].x, acc.y + red[v][c][lane].y);
+        e[v] = acc;
+    }
+    double2 o[3];
+#pragma unroll
+    for (int v = 0; v < 3; ++v) o[v] = make_double2(__shfl_xor(e[v].x, 1), __shfl_xor(e[v].y, 1));
+    const double2* e1 = ap ? o : e;   // a = 1
+    const double2* e2 = ap ? e : o;   // a = 2
+    auto lam = [&](int kind, int aa, int t3) { return a.lam[(kind * 2 + aa) * 3 + t3]; };
+    auto add2 = [](double2 x, double2 y) { return make_double2(x.x + y.x, x.y + y.y); };
+    const double2 h0 = add2(cmul(lam(0, 0, 0), e1[0]), cmul(lam(0, 1, 0), e2[0]));       // r2 = 0
+    const double2 h257 = add2(cmul(lam(1, 0, 0), e1[0]), cmul(lam(1, 1, 0), e2[0]));
+    const double2 h512 = add2(cmul(lam(1, 0, 0), e1[1]), cmul(lam(1, 1, 0), e2[1]));     // r2 = 255, t = 0
+    const double2 h513 = add2(cmul(lam(1, 0, 1), e1[2]), cmul(lam(1, 1, 1), e2[2]));     // r2 = 256, t = 1
+    const double p511 = a.phi[511], p0 = a.phi[0], p256 = a.phi[256], p257 = a.phi[257];
+    const double2 c1 = h513;
+    const double2 c0 = make_double2(h512.x - c1.x * p511, h512.y - c1.y * p511);
+    if (!live) return;
+    if (ap == 0) {
+        a.C[p] = make_double2(h0.x - c0.x * p0, h0.y - c0.y * p0);
+        ((double2*)a.cc)[2ull * p] = c0;
+        ((double2*)a.cc)[2ull * p + 1] = c1;
+    } else {
+        a.C[257ull * a.scM + p] = make_double2(h257.x - c0.x * p257 - c1.x * p256, h257.y - c0.y * p257 - c1.y * p256);
+    }
+}
+
+int launch_cwdft_inv_dots(const CGemmArgs& a, const double2* in, const double2* xpow, hipStream_t s) {
+    hipLaunchKernelGGL(cwdft_inv_dots_kernel, dim3((a.Pf + 15) / 16), dim3(256), 0, s, a, in, xpow);
+    MFHE_CHECK_LAUNCH("cwdft_inv_dots_kernel");
+    return MFHE_OK;
 }
 
 // ---------------- i8 MFMA modular GEMM (W-CRT, M = K = 512) ----------------
@@ -1067,7 +1219,9 @@ int launch_mod_gemm(const ModGemmArgs& a, int L, hipStream_t s) {
 int launch_cgemm(const CGemmArgs& a, int batch, hipStream_t s) {
     dim3 grid((a.P + TP - 1) / TP, (a.M + TM - 1) / TM, batch);
     if (a.mfma) {
-        hipLaunchKernelGGL(cgemm_mfma_kernel, grid, dim3(NTH), 0, s, a);
+        if (a.fac == 1) hipLaunchKernelGGL(cgemm_mfma_kernel<1>, grid, dim3(NTH), 0, s, a);
+        else if (a.fac == 2) hipLaunchKernelGGL(cgemm_mfma_kernel<2>, grid, dim3(NTH), 0, s, a);
+        else hipLaunchKernelGGL(cgemm_mfma_kernel<0>, grid, dim3(NTH), 0, s, a);
         MFHE_CHECK_LAUNCH("cgemm_mfma_kernel");
     } else {
         hipLaunchKernelGGL(cgemm_kernel, grid, dim3(NTH), 0, s, a);

@@ -66,9 +66,21 @@ struct CGemmArgs {
     int M, K, log_n;
     uint32_t P;
     bool mfma = true;      // f64 MFMA kernel; false = VALU mul-then-add kernel (oracle term order)
+    // factored W-DFT (gemm.hip, 771 = 3 x 257, as the W-CRT): 0 dense; 1 forward: A = Z [256][256], B read as
+    // F_a[k + 1] folded from in[k + 1], in[k + 258] on load, columns a' Pf + p, rows of C a' 256 + m, plus F_a[0];
+    // 2 inverse: A = Z^-1, B = in[a' 256 + k][p] in interleaved columns 2 p + a', epilogue lam / Phi_771 as the
+    // integer inverse (rows 0 and 257 and (c0, c1) come from cwdft_inv_dots_kernel).  in / out row-major [512][Pf].
+    int fac = 0;
+    uint32_t Pf = 0;
+    const double2* cc = nullptr;    // fac 2: [Pf][2] (c0, c1)
+    const double2* lam = nullptr;   // fac 2: [2: lam1, lam2][2: a'][3: t]
+    const int8_t* phi = nullptr;    // fac 2: [513] Phi_771 coefficients
 };
 
 int launch_mod_gemm(const ModGemmArgs& a, int L, hipStream_t s);
 int launch_cgemm(const CGemmArgs& a, int batch, hipStream_t s);
+// factored inverse W-DFT, first step: per column the rows r2 = 0, 255, 256 of E_a by dot products (xpow [2][256]:
+// zeta^(-255 b), zeta^(-256 b)), then f_0, f_257 into out and (c0, c1) into a.cc (gemm.hip)
+int launch_cwdft_inv_dots(const CGemmArgs& a, const double2* in, const double2* xpow, hipStream_t s);
 
 }  // namespace mfhe

@@ -623,9 +623,41 @@ static int wcrt_gemm(mfhe_ctx* c, const uint64_t* A, const uint64_t* B, bool b_p
     return launch_mod_gemm(a, g.L, s);
 }
 
-// complex W-DFT / W-IDFT over [phi][n2]
-static int wdft(const mfhe_ctx* c, const double2* A, const double2* in, double2* out, hipStream_t s) {
+// complex W-DFT / W-IDFT over [phi][n2]; MFHE_OPT_CGEMM_MFMA = 2 (default): factored through 771 = 3 x 257
+// (gemm.hip cgemm_mfma_kernel<1 / 2>), half the flops of the dense 512 x 512 product
+static int wdft(mfhe_ctx* c, const double2* A, const double2* in, double2* out, hipStream_t s) {
     const Geo2 g = geo(c);
+    if (c->cgemm_mfma == 2 && c->d_wdZ && (A == c->d_wdV || A == c->d_wdVinv)) {
+        CGemmArgs f;
+        f.mfma = true;
+        f.B = in;
+        f.C = out;
+        f.aB = f.bB = f.cB = 0;
+        f.M = f.K = 256;
+        f.Pf = (uint32_t)g.n2;
+        f.P = 2 * f.Pf;
+        f.scM = g.n2;
+        if (A == c->d_wdV) {
+            f.fac = 1;
+            f.A = c->d_wdZ;
+            return launch_cgemm(f, 1, s);
+        }
+        const size_t need = (size_t)g.n2 * 2 * sizeof(double2);
+        if (c->wd_ws_bytes < need) {
+            if (c->wd_ws) MFHE_HIP(hipFree(c->wd_ws));
+            c->wd_ws = nullptr;
+            c->wd_ws_bytes = 0;
+            MFHE_HIP(hipMalloc(&c->wd_ws, need));
+            c->wd_ws_bytes = need;
+        }
+        f.fac = 2;
+        f.A = c->d_wdZi;
+        f.cc = (const double2*)c->wd_ws;
+        f.lam = c->d_wdlam;
+        f.phi = c->d_wdphi;
+        RC(launch_cwdft_inv_dots(f, in, c->d_wdxp, s));
+        return launch_cgemm(f, 1, s);
+    }
     CGemmArgs a;
     a.mfma = c->cgemm_mfma != 0;
     a.A = A; a.B = in; a.C = out;

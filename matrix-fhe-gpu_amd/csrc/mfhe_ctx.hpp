@@ -105,7 +105,7 @@ struct mfhe_ctx {
                                  // phi_r2, phi_(r2-1), phi_(r2+257), phi_(r2+256) as (value + 1) at bits 0, 2, 4, 6
     int wcrt_mfma = 1;           // MFHE_OPT_WCRT_MFMA
     int wcrt_pipe = 0;           // MFHE_OPT_WCRT_PIPE
-    int cgemm_mfma = 1;          // MFHE_OPT_CGEMM_MFMA
+    int cgemm_mfma = 2;          // MFHE_OPT_CGEMM_MFMA
     int he_fused = 1;            // MFHE_OPT_HE_FUSED
     int limb_base = 0;           // residue shard: global index of this context's limb 0 (mfhe_ctx_set_limb_shard)
     int limbs_total = 0;         // residue shard: L of the whole parameter set (0 = this context's L)
@@ -145,6 +145,14 @@ struct mfhe_ctx {
     uint64_t* d_wVinv = nullptr;   // [L][512][512]  V_l^-1[r][w] (row-major)
     double2* d_wdV = nullptr;      // [512][512]     complex W-DFT
     double2* d_wdVinv = nullptr;   // [512][512]     its inverse (complex Gauss-Jordan)
+    // factored W-DFT (MFHE_OPT_CGEMM_MFMA = 2, gemm.hip): zeta = e^(2 pi i / 257)
+    double2* d_wdZ = nullptr;      // [256][256] zeta^((i+1)(k+1))
+    double2* d_wdZi = nullptr;     // [256][256] zeta^-((i+1)(k+1))
+    double2* d_wdlam = nullptr;    // [2][2][3]  lam1 / lam2 [a'][t] of the inverse (771^-1 omega^-at differences)
+    double2* d_wdxp = nullptr;     // [2][256]   zeta^(-255 b), zeta^(-256 b), b = 1..256
+    int8_t* d_wdphi = nullptr;     // [513]      Phi_771 coefficients
+    void* wd_ws = nullptr;         // factored inverse W-DFT (c0, c1) per column, grown on demand
+    size_t wd_ws_bytes = 0;
     double2 *d_encV = nullptr, *d_encVT = nullptr, *d_encVi = nullptr, *d_encViT = nullptr;  // [n][n]
 
     int trace_split = 2;              // MFHE_OPT_TRACE_SPLIT: split-digit kernel (2 MFMA, 1 VALU) when every q < 2^45
