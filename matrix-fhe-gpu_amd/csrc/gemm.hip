@@ -205,9 +205,10 @@ __global__ __launch_bounds__(NTH, 2) void cgemm_mfma_kernel(CGemmArgs a) {
                 rb[e] = (k < a.K && p < a.P) ? B[b_off(k, p, a.sbK, a.sbY, a.log_n)] : make_double2(0, 0);
             } else if constexpr (FAC == 1) {
                 // F_a[r2] = omega^(a t) in[r2] + omega^(a ((t + 2) mod 3)) in[r2 + 257], r2 = k + 1, t = r2 mod 3
+                // interleaved columns 2 p + a': lanes 2p, 2p + 1 load the same two inputs (one fetch per pair)
                 const bool live = p < a.P;
-                const int ap = p >= a.Pf;
-                const uint32_t pc = live ? p - ap * a.Pf : 0;
+                const int ap = p & 1;
+                const uint32_t pc = live ? p >> 1 : 0;
                 const int r2 = k + 1, t3 = r2 % 3, r3 = r2 + 257 < 512 ? r2 + 257 : 511;
                 const double2 x1 = B[(uint64_t)r2 * a.Pf + pc], x2 = B[(uint64_t)r3 * a.Pf + pc];
                 const double2 f1 = cmul(omega3(((ap + 1) * t3) % 3), x1);
@@ -289,8 +290,8 @@ __global__ __launch_bounds__(NTH, 2) void cgemm_mfma_kernel(CGemmArgs a) {
         for (int j = 0; j < 2; ++j) {
             const uint32_t c = p0 + wp + 16 * j + r;
             if (c >= a.P) continue;
-            const int ap = c >= a.Pf;
-            const uint32_t p = c - ap * a.Pf;
+            const int ap = c & 1;
+            const uint32_t p = c >> 1;
             const double2 f = cmul(omega3((2 * (ap + 1)) % 3), B[257ull * a.Pf + p]), x0 = B[p];
             const double2 add = make_double2(x0.x + f.x, x0.y + f.y);
 #pragma unroll

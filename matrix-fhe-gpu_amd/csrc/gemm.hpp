@@ -67,7 +67,7 @@ struct CGemmArgs {
     uint32_t P;
     bool mfma = true;      // f64 MFMA kernel; false = VALU mul-then-add kernel (oracle term order)
     // factored W-DFT (gemm.hip, 771 = 3 x 257, as the W-CRT): 0 dense; 1 forward: A = Z [256][256], B read as
-    // F_a[k + 1] folded from in[k + 1], in[k + 258] on load, columns a' Pf + p, rows of C a' 256 + m, plus F_a[0];
+    // F_a[k + 1] folded from in[k + 1], in[k + 258] on load, columns 2 p + a', rows of C a' 256 + m, plus F_a[0];
     // 2 inverse: A = Z^-1, B = in[a' 256 + k][p] in interleaved columns 2 p + a', epilogue lam / Phi_771 as the
     // integer inverse (rows 0 and 257 and (c0, c1) come from cwdft_inv_dots_kernel).  in / out row-major [512][Pf].
     int fac = 0;
