@@ -12,4 +12,6 @@ timeout -s KILL 120 rocprofv3 --pmc SQ_VALU_MFMA_BUSY_CYCLES SQ_BUSY_CYCLES SQ_W
     python3 "$ROOT/tools/pipeline_bench.py" 3 > "$OUT/pmc.log" 2>&1 || { echo "pmc failed rc=$?"; tail -5 "$OUT/pmc.log"; exit 5; }
 python3 "$ROOT/tools/gemm_pmc_summary.py" "$OUT/pmc" gemm | tee "$OUT/summary.txt"
 python3 "$ROOT/tools/gemm_pmc_summary.py" "$OUT/pmc" digitize | tee -a "$OUT/summary.txt"
+python3 "$ROOT/tools/gemm_pmc_summary.py" "$OUT/pmc" ring_kernel | tee -a "$OUT/summary.txt"
+python3 "$ROOT/tools/gemm_pmc_summary.py" "$OUT/pmc" cwdft | tee -a "$OUT/summary.txt"
 exit 0
