@@ -507,16 +507,23 @@ constexpr int FK = 256;   // K (and M) of the factored GEMM
 // 16-byte store completes a 1 KiB contiguous run per wave.  The digits need any representative of F_a mod q
 // within the limb's digit range, so F_a is only reduced to the centred (-q/2, q/2] and split by the offset
 // rule (balanced_bytes).
-template <int D>
-__global__ __launch_bounds__(256) void mfma_digitize_fold_kernel(const uint64_t* __restrict__ B, uint64_t bL,
+// QF (encode): B is not a residue matrix but the W-IDFT's doubles v[r][p] (row stride qf_row, element stride
+// qf_step): each limb's residue is formed on the fly as round(v delta) mod q -- the RNS decompose
+// (rns_decompose_kernel: llround, then the residue of the int64) fused away, exact for |v delta| < 2^63 (the
+// centred FP64 reduction of the rounded double is exact while |x / q| < 2^51).  The grid then runs the limbs
+// fastest (blockIdx.x), so the L blocks of one column range read the same doubles out of the L2.
+template <int D, bool QF = false>
+__global__ __launch_bounds__(256, 4) void mfma_digitize_fold_kernel(const uint64_t* __restrict__ B, uint64_t bL,
                                                                  uint64_t sbK, uint64_t sbY, int log_n, uint32_t P,
                                                                  uint32_t Ppad, const double* __restrict__ fold,
                                                                  int8_t* __restrict__ out, uint64_t* __restrict__ d0,
-                                                                 PlaneCounts pc) {
-    const uint32_t p = blockIdx.x * 128 + (threadIdx.x >> 1);
+                                                                 PlaneCounts pc, const double* __restrict__ qf = nullptr,
+                                                                 uint64_t qf_row = 0, uint64_t qf_step = 0,
+                                                                 double delta = 0.0) {
+    const uint32_t p = (QF ? blockIdx.y : blockIdx.x) * 128 + (threadIdx.x >> 1);
     const int hf = threadIdx.x & 1;
-    const int kc = blockIdx.y;   // panel: r2 = 32 kc + 16 hf + 1 .. 32 kc + 16 hf + 16
-    const int l = blockIdx.z;
+    const int kc = QF ? blockIdx.z : blockIdx.y;   // panel: r2 = 32 kc + 16 hf + 1 .. 32 kc + 16 hf + 16
+    const int l = QF ? blockIdx.x : blockIdx.z;
     if (p >= Ppad) return;
     const double* fo = fold + (uint64_t)l * 16;
     LimbConst lc;
@@ -537,7 +544,12 @@ __global__ __launch_bounds__(256) void mfma_digitize_fold_kernel(const uint64_t*
     // unconditional loads (column 0 stands in for the padding columns, then zeroed): a load under `live ? :` is
     // a branch per load, each followed by its own vmcnt(0) -- the 32 loads of a thread ran one at a time
     const uint64_t cl = live ? col : 0;
-    auto in = [&](int r) { const double x = ArithF64::from_u64(Bl[(uint64_t)r * sbK + cl]); return live ? x : 0.0; };
+    auto in = [&](int r) {
+        double x;
+        if constexpr (QF) x = ar.reduce(round(qf[(uint64_t)r * qf_row + (uint64_t)(live ? p : 0) * qf_step] * delta));
+        else x = ArithF64::from_u64(Bl[(uint64_t)r * sbK + cl]);
+        return live ? x : 0.0;
+    };
     uint32_t pk[2][D][4];
 #pragma unroll
     for (int ap = 0; ap < 2; ++ap)
@@ -1097,10 +1109,21 @@ static int launch_factored(const ModGemmArgs& a, int L, hipStream_t s) {
     f.d0 = (uint64_t*)(a.Bdig + (size_t)L * a.D * Ppad * MK);
     const dim3 gd((Ppad + 127) / 128, FK / 32, L);
     const PlaneCounts pc = plane_counts(a, L);
-    if (a.D == 5) hipLaunchKernelGGL(mfma_digitize_fold_kernel<5>, gd, dim3(256), 0, s, a.B, a.bL, a.sbK, a.sbY, a.log_n,
-                                     a.P, Ppad, a.fold, a.Bdig, f.d0, pc);
-    else hipLaunchKernelGGL(mfma_digitize_fold_kernel<6>, gd, dim3(256), 0, s, a.B, a.bL, a.sbK, a.sbY, a.log_n, a.P,
-                            Ppad, a.fold, a.Bdig, f.d0, pc);
+    if (a.qf) {
+        const dim3 gq(L, (Ppad + 127) / 128, FK / 32);
+        if (a.D == 5)
+            hipLaunchKernelGGL((mfma_digitize_fold_kernel<5, true>), gq, dim3(256), 0, s, a.B, a.bL, a.sbK, a.sbY,
+                               a.log_n, a.P, Ppad, a.fold, a.Bdig, f.d0, pc, a.qf, a.qf_row, a.qf_step, a.delta);
+        else
+            hipLaunchKernelGGL((mfma_digitize_fold_kernel<6, true>), gq, dim3(256), 0, s, a.B, a.bL, a.sbK, a.sbY,
+                               a.log_n, a.P, Ppad, a.fold, a.Bdig, f.d0, pc, a.qf, a.qf_row, a.qf_step, a.delta);
+    } else if (a.D == 5) {
+        hipLaunchKernelGGL(mfma_digitize_fold_kernel<5>, gd, dim3(256), 0, s, a.B, a.bL, a.sbK, a.sbY, a.log_n,
+                           a.P, Ppad, a.fold, a.Bdig, f.d0, pc);
+    } else {
+        hipLaunchKernelGGL(mfma_digitize_fold_kernel<6>, gd, dim3(256), 0, s, a.B, a.bL, a.sbK, a.sbY, a.log_n, a.P,
+                           Ppad, a.fold, a.Bdig, f.d0, pc);
+    }
     MFHE_CHECK_LAUNCH("mfma_digitize_fold_kernel");
     for (int l0 = 0; l0 < L;) {
         const int d = a.limbD ? std::max(a.limbD[l0], 5) : a.D;

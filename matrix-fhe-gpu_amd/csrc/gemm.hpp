@@ -50,6 +50,11 @@ struct ModGemmArgs {
     const double* iz = nullptr;
     const uint8_t* phi = nullptr;
     double* cc = nullptr;        // set by the launcher: [L][Ppad][2] (c0, c1) per column (the d0 workspace)
+    // factored forward only: B given as the doubles v[r][p] at qf[r * qf_row + p * qf_step], residues
+    // round(v delta) mod q formed in the digitize kernel (the encode's RNS decompose fused away); null = B
+    const double* qf = nullptr;
+    uint64_t qf_row = 0, qf_step = 0;
+    double delta = 0.0;
 };
 
 // bytes of B digit workspace the MFMA path needs for P columns and L limbs at D digits

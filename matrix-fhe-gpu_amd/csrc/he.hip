@@ -595,8 +595,13 @@ static int use_mfma(mfhe_ctx* c, ModGemmArgs& a, const uint64_t* A, int L) {
     return MFHE_OK;
 }
 
+// qf (encode): B replaced by the W-IDFT's doubles, quantized and reduced inside the factored forward's digitize
+// kernel (gemm.hip mfma_digitize_fold_kernel<D, true>); only when quant_fused_ok(c)
+static bool quant_fused_ok(const mfhe_ctx* c) {
+    return c->wcrt_mfma == 1 && c->wD && c->d_wZdig && c->d_wepi && c->d_wfold;
+}
 static int wcrt_gemm(mfhe_ctx* c, const uint64_t* A, const uint64_t* B, bool b_poly, uint64_t* C, WOut out,
-                     bool vector, hipStream_t s) {
+                     bool vector, hipStream_t s, const double* qf = nullptr, uint64_t qf_step = 0) {
     const Geo2 g = geo(c);
     ModGemmArgs a;
     a.A = A;
@@ -620,6 +625,13 @@ static int wcrt_gemm(mfhe_ctx* c, const uint64_t* A, const uint64_t* B, bool b_p
         else { a.cL = g.n2; a.scM = (uint64_t)g.L * g.n2; a.scY = g.n; }
     }
     RC(use_mfma(c, a, A, g.L));
+    if (qf) {
+        if (!a.fold) return set_error(MFHE_EINVAL, "W-CRT: fused quantization needs the factored forward");
+        a.qf = qf;
+        a.qf_row = g.n2 * qf_step;
+        a.qf_step = qf_step;
+        a.delta = c->delta;
+    }
     return launch_mod_gemm(a, g.L, s);
 }
 
@@ -709,7 +721,13 @@ static int encode_impl(mfhe_ctx* c, const double* msg, uint64_t* out_re, uint64_
     RC(xy3(c, c->d_encVi, (const double2*)msg, c->d_encViT, tmp, xy, 512, s));
     // 2) W-IDFT (w_idft_kernel, batched_encoder.cu:104-123)
     RC(wdft(c, c->d_wdVinv, xy, tmp, s));
-    // 3) quantize + RNS split, 4) W-CRT -> matrix-major eval (re, then im)
+    // 3) quantize + RNS split, 4) W-CRT -> matrix-major eval (re, then im); fused into the W-CRT's digitize
+    // kernel when the factored forward runs (the residues never reach HBM)
+    if (quant_fused_ok(c)) {
+        RC(wcrt_gemm(c, c->d_wV, (const uint64_t*)tmp, false, out_re, WOut::Matrix, false, s, (const double*)tmp, 2));
+        RC(wcrt_gemm(c, c->d_wV, (const uint64_t*)tmp, false, out_im, WOut::Matrix, false, s, (const double*)tmp + 1, 2));
+        return MFHE_OK;
+    }
     RC(mfhe_rns_decompose(c, (const double*)tmp, 2, 512, g.n2, cre, (mfhe_stream_t)s));
     RC(wcrt_gemm(c, c->d_wV, cre, false, out_re, WOut::Matrix, false, s));
     RC(mfhe_rns_decompose(c, (const double*)tmp + 1, 2, 512, g.n2, cre, (mfhe_stream_t)s));
