@@ -36,6 +36,9 @@
 #ifndef MFHE_NTT_NGB17
 #define MFHE_NTT_NGB17 4    // N = 2^17 forward: 512-element rows per block-pass workgroup (8 -> 4: +0.9% C5 shard)
 #endif
+#ifndef MFHE_NTT_INV17_SPLIT
+#define MFHE_NTT_INV17_SPLIT 0      // N = 2^17 inverse: 0 = 8 block + 9 column stages; 1 = 9 block + 8 column (DMA pass)
+#endif
 #ifndef MFHE_NTT_INV16_PLAIN_NG
 #define MFHE_NTT_INV16_PLAIN_NG 0   // N = 2^16 inverse last pass: 0 = DMA column pass; 16 / 32 = plain column pass (A/B)
 #endif
@@ -352,7 +355,8 @@ static int run_phantom(const NttJob<TS>& j, hipStream_t st) {
         // pass 9; the inverse keeps 9 column + 8 block stages.  Measured per direction (profiles/r02_n17_split.txt):
         // forward +5%, inverse -2.5% with the other split.
         case 17:
-            if constexpr (INV) return two_pass<A, TS, 9, MFHE_NTT_NGA17I, 8, MFHE_NTT_NGB17I, INV>(j, st);
+            if constexpr (INV && MFHE_NTT_INV17_SPLIT == 1) return two_pass<A, TS, 8, 16, 9, MFHE_NTT_NGB17, INV>(j, st);
+            else if constexpr (INV) return two_pass<A, TS, 9, MFHE_NTT_NGA17I, 8, MFHE_NTT_NGB17I, INV>(j, st);
             else return two_pass<A, TS, 8, 16, 9, MFHE_NTT_NGB17, INV>(j, st);
         default: return set_error(MFHE_EUNSUPPORTED, "NTT supports log_n <= 17");
     }
