@@ -507,19 +507,30 @@ constexpr int FK = 256;   // K (and M) of the factored GEMM
 // 16-byte store completes a 1 KiB contiguous run per wave.  The digits need any representative of F_a mod q
 // within the limb's digit range, so F_a is only reduced to the centred (-q/2, q/2] and split by the offset
 // rule (balanced_bytes).
-// QF (encode): B is not a residue matrix but the W-IDFT's doubles v[r][p] (row stride qf_row, element stride
+// SRC 1 (encode): B is not a residue matrix but the W-IDFT's doubles v[r][p] (row stride qf_row, element stride
 // qf_step): each limb's residue is formed on the fly as round(v delta) mod q -- the RNS decompose
 // (rns_decompose_kernel: llround, then the residue of the int64) fused away, exact for |v delta| < 2^63 (the
-// centred FP64 reduction of the rounded double is exact while |x / q| < 2^51).  The grid then runs the limbs
-// fastest (blockIdx.x), so the L blocks of one column range read the same doubles out of the L2.
-template <int D, bool QF = false>
+// centred FP64 reduction of the rounded double is exact while |x / q| < 2^51).  With any SRC the grid runs the
+// limbs fastest (blockIdx.x), so the L blocks of one column range read the same doubles out of the L2.
+// SRC 2 / 3 (encrypt): the uniform sampler's residue computed in place (seed from (w, limb, position) exactly as
+// he.hip uniform_kernel, so no a[] in HBM), or the Gaussian noise read as one centred integer per coefficient.
+struct FoldSrc {
+    const double* qf = nullptr;
+    uint64_t qf_row = 0, qf_step = 0;
+    double delta = 0.0;
+    const uint64_t* qmu = nullptr;   // SRC 2: [L][2] (q, floor(2^64 / q))
+    int lbase = 0, Ltot = 0;
+};
+template <int D, int SRC = 0>
 __global__ __launch_bounds__(256, 4) void mfma_digitize_fold_kernel(const uint64_t* __restrict__ B, uint64_t bL,
                                                                  uint64_t sbK, uint64_t sbY, int log_n, uint32_t P,
                                                                  uint32_t Ppad, const double* __restrict__ fold,
                                                                  int8_t* __restrict__ out, uint64_t* __restrict__ d0,
-                                                                 PlaneCounts pc, const double* __restrict__ qf = nullptr,
-                                                                 uint64_t qf_row = 0, uint64_t qf_step = 0,
-                                                                 double delta = 0.0) {
+                                                                 PlaneCounts pc, FoldSrc fs = FoldSrc{}) {
+    constexpr bool QF = SRC != 0;
+    const double* __restrict__ qf = fs.qf;
+    const uint64_t qf_row = fs.qf_row, qf_step = fs.qf_step;
+    const double delta = fs.delta;
     const uint32_t p = (QF ? blockIdx.y : blockIdx.x) * 128 + (threadIdx.x >> 1);
     const int hf = threadIdx.x & 1;
     const int kc = QF ? blockIdx.z : blockIdx.y;   // panel: r2 = 32 kc + 16 hf + 1 .. 32 kc + 16 hf + 16
@@ -544,10 +555,28 @@ __global__ __launch_bounds__(256, 4) void mfma_digitize_fold_kernel(const uint64
     // unconditional loads (column 0 stands in for the padding columns, then zeroed): a load under `live ? :` is
     // a branch per load, each followed by its own vmcnt(0) -- the 32 loads of a thread ran one at a time
     const uint64_t cl = live ? col : 0;
+    uint64_t uq = 0, umu = 0;
+    if constexpr (SRC == 2) {
+        uq = fs.qmu[2 * l];
+        umu = fs.qmu[2 * l + 1];
+    }
     auto in = [&](int r) {
         double x;
-        if constexpr (QF) x = ar.reduce(round(qf[(uint64_t)r * qf_row + (uint64_t)(live ? p : 0) * qf_step] * delta));
-        else x = ArithF64::from_u64(Bl[(uint64_t)r * sbK + cl]);
+        const uint32_t pp = live ? p : 0;
+        if constexpr (SRC == 1) {
+            x = ar.reduce(round(qf[(uint64_t)r * qf_row + (uint64_t)pp * qf_step] * delta));
+        } else if constexpr (SRC == 2) {
+            uint64_t seed = 123456789ULL + (((uint64_t)r * (uint64_t)fs.Ltot + (uint64_t)(fs.lbase + l)) << (2 * log_n)) + pp;
+            seed = seed * 6364136223846793005ULL + 1442695040888963407ULL;
+            uint64_t v = seed - __umul64hi(seed, umu) * uq;   // Barrett as uniform_kernel: [0, 3q)
+            v = v >= uq ? v - uq : v;
+            v = v >= uq ? v - uq : v;
+            x = ArithF64::from_u64(v);
+        } else if constexpr (SRC == 3) {
+            x = qf[(uint64_t)r * qf_row + pp];
+        } else {
+            x = ArithF64::from_u64(Bl[(uint64_t)r * sbK + cl]);
+        }
         return live ? x : 0.0;
     };
     uint32_t pk[2][D][4];
@@ -1109,14 +1138,24 @@ static int launch_factored(const ModGemmArgs& a, int L, hipStream_t s) {
     f.d0 = (uint64_t*)(a.Bdig + (size_t)L * a.D * Ppad * MK);
     const dim3 gd((Ppad + 127) / 128, FK / 32, L);
     const PlaneCounts pc = plane_counts(a, L);
-    if (a.qf) {
+    if (a.qsrc) {
+        FoldSrc fs;
+        fs.qf = a.qf;
+        fs.qf_row = a.qf_row;
+        fs.qf_step = a.qf_step;
+        fs.delta = a.delta;
+        fs.qmu = a.qmu;
+        fs.lbase = a.lbase;
+        fs.Ltot = a.Ltot;
         const dim3 gq(L, (Ppad + 127) / 128, FK / 32);
-        if (a.D == 5)
-            hipLaunchKernelGGL((mfma_digitize_fold_kernel<5, true>), gq, dim3(256), 0, s, a.B, a.bL, a.sbK, a.sbY,
-                               a.log_n, a.P, Ppad, a.fold, a.Bdig, f.d0, pc, a.qf, a.qf_row, a.qf_step, a.delta);
-        else
-            hipLaunchKernelGGL((mfma_digitize_fold_kernel<6, true>), gq, dim3(256), 0, s, a.B, a.bL, a.sbK, a.sbY,
-                               a.log_n, a.P, Ppad, a.fold, a.Bdig, f.d0, pc, a.qf, a.qf_row, a.qf_step, a.delta);
+#define MFHE_FOLD_SRC(d, src)                                                                                    \
+    hipLaunchKernelGGL((mfma_digitize_fold_kernel<d, src>), gq, dim3(256), 0, s, a.B, a.bL, a.sbK, a.sbY, a.log_n, \
+                       a.P, Ppad, a.fold, a.Bdig, f.d0, pc, fs)
+        if (a.qsrc == 1) { if (a.D == 5) MFHE_FOLD_SRC(5, 1); else MFHE_FOLD_SRC(6, 1); }
+        else if (a.qsrc == 2) { if (a.D == 5) MFHE_FOLD_SRC(5, 2); else MFHE_FOLD_SRC(6, 2); }
+        else if (a.qsrc == 3) { if (a.D == 5) MFHE_FOLD_SRC(5, 3); else MFHE_FOLD_SRC(6, 3); }
+        else return set_error(MFHE_EINVAL, "mod_gemm: unknown digitize source");
+#undef MFHE_FOLD_SRC
     } else if (a.D == 5) {
         hipLaunchKernelGGL(mfma_digitize_fold_kernel<5>, gd, dim3(256), 0, s, a.B, a.bL, a.sbK, a.sbY, a.log_n,
                            a.P, Ppad, a.fold, a.Bdig, f.d0, pc);

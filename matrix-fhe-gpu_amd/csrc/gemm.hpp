@@ -50,11 +50,16 @@ struct ModGemmArgs {
     const double* iz = nullptr;
     const uint8_t* phi = nullptr;
     double* cc = nullptr;        // set by the launcher: [L][Ppad][2] (c0, c1) per column (the d0 workspace)
-    // factored forward only: B given as the doubles v[r][p] at qf[r * qf_row + p * qf_step], residues
-    // round(v delta) mod q formed in the digitize kernel (the encode's RNS decompose fused away); null = B
+    // factored forward only: where the digitize kernel takes B from (gemm.hip mfma_digitize_fold_kernel<D, SRC>)
+    //  qsrc 0: B (residues); 1: the doubles v[r][p] at qf[r * qf_row + p * qf_step], residue round(v delta) mod q
+    //  (the encode's RNS decompose fused away); 2: the encrypt's uniform sampler (he.hip uniform_kernel) evaluated
+    //  in place, limb lbase + l of Ltot; 3: one centred integer per (r, p) at qf[r * qf_row + p] (the Gaussian
+    //  noise, drawn once per coefficient, he.hip gaussian_compact_kernel), the same integer in every limb
+    int qsrc = 0;
     const double* qf = nullptr;
     uint64_t qf_row = 0, qf_step = 0;
     double delta = 0.0;
+    int lbase = 0, Ltot = 0;
 };
 
 // bytes of B digit workspace the MFMA path needs for P columns and L limbs at D digits

@@ -103,6 +103,23 @@ __global__ void gaussian_kernel(uint64_t* e, const uint64_t* qmu, int L, int log
     }
 }
 
+// The same draw as gaussian_kernel, once per [w][y][x] as a centred integer in a double: the factored W-CRT's
+// digitize reads it for every limb (gemm.hip FoldSrc, qsrc 3), so the L-limb residue array never reaches HBM.
+__global__ void gaussian_compact_kernel(double* e, int log_n, uint64_t total) {
+    const uint64_t idx = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x;
+    if (idx >= total) return;
+    const uint64_t n2 = 1ull << (2 * log_n);
+    const uint64_t w = idx >> (2 * log_n), pos = idx & (n2 - 1);
+    const uint64_t r1 = splitmix64(0xD6E8FEB86659FD93ULL ^ (w * n2 + pos));
+    const uint64_t r2 = splitmix64(r1);
+    const double inv53 = 1.0 / 9007199254740992.0;
+    const double u1 = ((double)(r1 >> 11) + 1.0) * inv53;
+    const double u2 = ((double)(r2 >> 11) + 1.0) * inv53;
+    const double mag = 3.2 * sqrt(-2.0 * log(u1));
+    const double z = mag * cos(6.283185307179586 * u2);
+    e[idx] = (double)llround(z);
+}
+
 // ---------------- ring ops (poly-major [phi*n][L][n]) ----------------
 // pointwise_mul_s_kernel HE.cu:509-531: t = a * s[w][l][x], w = poly / n.  The reference reduces with
 // an __int128 % per element (a software division here too); this uses the exact FP64 modmul of the NTT
@@ -596,12 +613,12 @@ static int use_mfma(mfhe_ctx* c, ModGemmArgs& a, const uint64_t* A, int L) {
 }
 
 // qf (encode): B replaced by the W-IDFT's doubles, quantized and reduced inside the factored forward's digitize
-// kernel (gemm.hip mfma_digitize_fold_kernel<D, true>); only when quant_fused_ok(c)
+// kernel (gemm.hip mfma_digitize_fold_kernel<D, SRC>, and the encrypt samplers with it); only when quant_fused_ok(c)
 static bool quant_fused_ok(const mfhe_ctx* c) {
     return c->wcrt_mfma == 1 && c->wD && c->d_wZdig && c->d_wepi && c->d_wfold;
 }
 static int wcrt_gemm(mfhe_ctx* c, const uint64_t* A, const uint64_t* B, bool b_poly, uint64_t* C, WOut out,
-                     bool vector, hipStream_t s, const double* qf = nullptr, uint64_t qf_step = 0) {
+                     bool vector, hipStream_t s, int qsrc = 0, const double* qf = nullptr, uint64_t qf_step = 1) {
     const Geo2 g = geo(c);
     ModGemmArgs a;
     a.A = A;
@@ -625,12 +642,15 @@ static int wcrt_gemm(mfhe_ctx* c, const uint64_t* A, const uint64_t* B, bool b_p
         else { a.cL = g.n2; a.scM = (uint64_t)g.L * g.n2; a.scY = g.n; }
     }
     RC(use_mfma(c, a, A, g.L));
-    if (qf) {
-        if (!a.fold) return set_error(MFHE_EINVAL, "W-CRT: fused quantization needs the factored forward");
+    if (qsrc) {
+        if (!a.fold) return set_error(MFHE_EINVAL, "W-CRT: a fused digitize source needs the factored forward");
+        a.qsrc = qsrc;
         a.qf = qf;
         a.qf_row = g.n2 * qf_step;
         a.qf_step = qf_step;
         a.delta = c->delta;
+        a.lbase = c->limb_base;
+        a.Ltot = c->limbs_total ? c->limbs_total : g.L;
     }
     return launch_mod_gemm(a, g.L, s);
 }
@@ -724,8 +744,8 @@ static int encode_impl(mfhe_ctx* c, const double* msg, uint64_t* out_re, uint64_
     // 3) quantize + RNS split, 4) W-CRT -> matrix-major eval (re, then im); fused into the W-CRT's digitize
     // kernel when the factored forward runs (the residues never reach HBM)
     if (quant_fused_ok(c)) {
-        RC(wcrt_gemm(c, c->d_wV, (const uint64_t*)tmp, false, out_re, WOut::Matrix, false, s, (const double*)tmp, 2));
-        RC(wcrt_gemm(c, c->d_wV, (const uint64_t*)tmp, false, out_im, WOut::Matrix, false, s, (const double*)tmp + 1, 2));
+        RC(wcrt_gemm(c, c->d_wV, (const uint64_t*)tmp, false, out_re, WOut::Matrix, false, s, 1, (const double*)tmp, 2));
+        RC(wcrt_gemm(c, c->d_wV, (const uint64_t*)tmp, false, out_im, WOut::Matrix, false, s, 1, (const double*)tmp + 1, 2));
         return MFHE_OK;
     }
     RC(mfhe_rns_decompose(c, (const double*)tmp, 2, 512, g.n2, cre, (mfhe_stream_t)s));
@@ -791,14 +811,22 @@ static int encrypt_impl(mfhe_ctx* c, const uint64_t* m_re, const uint64_t* m_im,
     uint64_t* eev = b.get<uint64_t>(g.words);
     const uint64_t W = g.words;
     // shared a: W coeff -> W-CRT eval (poly-major) -> X-NTT
-    hipLaunchKernelGGL(uniform_kernel, g1(W), dim3(256), 0, s, ap, c->d_rns_mu, g.L, g.logn, W, c->limb_base,
-                       c->limbs_total ? c->limbs_total : g.L);
-    MFHE_CHECK_LAUNCH("uniform_kernel");
-    RC(wcrt_gemm(c, c->d_wV, ap, false, aev, WOut::Poly, false, s));
     // e: identical for re and im (seed depends only on the coefficient, HE.cu:605-608)
-    hipLaunchKernelGGL(gaussian_kernel, g1(W / g.L), dim3(256), 0, s, ep, c->d_rns_mu, g.L, g.logn, W / g.L);
-    MFHE_CHECK_LAUNCH("gaussian_kernel");
-    RC(wcrt_gemm(c, c->d_wV, ep, false, eev, WOut::Poly, false, s));
+    if (quant_fused_ok(c)) {
+        // the samplers evaluated inside the factored W-CRT's digitize: a in place, e from one draw per coefficient
+        RC(wcrt_gemm(c, c->d_wV, ap, false, aev, WOut::Poly, false, s, 2));
+        hipLaunchKernelGGL(gaussian_compact_kernel, g1(W / g.L), dim3(256), 0, s, (double*)ep, g.logn, W / g.L);
+        MFHE_CHECK_LAUNCH("gaussian_compact_kernel");
+        RC(wcrt_gemm(c, c->d_wV, ep, false, eev, WOut::Poly, false, s, 3, (const double*)ep, 1));
+    } else {
+        hipLaunchKernelGGL(uniform_kernel, g1(W), dim3(256), 0, s, ap, c->d_rns_mu, g.L, g.logn, W, c->limb_base,
+                           c->limbs_total ? c->limbs_total : g.L);
+        MFHE_CHECK_LAUNCH("uniform_kernel");
+        RC(wcrt_gemm(c, c->d_wV, ap, false, aev, WOut::Poly, false, s));
+        hipLaunchKernelGGL(gaussian_kernel, g1(W / g.L), dim3(256), 0, s, ep, c->d_rns_mu, g.L, g.logn, W / g.L);
+        MFHE_CHECK_LAUNCH("gaussian_kernel");
+        RC(wcrt_gemm(c, c->d_wV, ep, false, eev, WOut::Poly, false, s));
+    }
     if (ring_fused_ok(c, g.logn)) {
         const uint64_t rows = W / g.n;
         const RingArgs ra = ring_args(c, sk, g.L, rows);
