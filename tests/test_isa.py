@@ -78,3 +78,28 @@ def test_column_pass_dma_waits_match_the_instruction_mix(inv, arith):
     assert not any("vmcnt" in l for l in lines[b0 + 1:s0]), [l for l in lines[b0 + 1:s0] if "vmcnt" in l]
     # the stores' base is uniform: no readfirstlane (waterfall) loop around them
     assert "s_cbranch_execnz" not in "\n".join(lines[s0:s0 + 80]), "stores wrapped in a waterfall loop"
+
+
+@pytest.mark.parametrize("kernel", [
+    r"_ZN4mfhe25mfma_digitize_fold_kernelILi5ELi0E[^>]*",
+    r"_ZN4mfhe25mfma_digitize_fold_kernelILi5ELi1E[^>]*",
+    r"_ZN4mfhe25mfma_digitize_fold_kernelILi5ELi3E[^>]*",
+    r"_ZN4mfhe26mfma_digitize_ifold_kernelILi5E[^>]*",
+])
+def test_digitize_loads_are_not_serialised(kernel):
+    """The W-CRT digitize kernels (gemm.hip) must keep their column loads in flight together: a load under a
+    `live ? x : 0` branch compiled to one branch per load, each followed by its own `s_waitcnt vmcnt(0)`, and a
+    thread's 32 loads ran one at a time (70 -> 45 us once fixed).  Pinned here: no global load
+    is followed by a vmcnt(0) within the next four instructions.  (The uniform-sampler source, SRC 2, computes its
+    values and loads nothing.)"""
+    asm = _kernel_asm(kernel)
+    lines = [ln for ln in asm.splitlines() if re.match(r"^\s+[0-9a-f]+:", ln) or ln.startswith("\t")]
+    serial = 0
+    loads = 0
+    for i, ln in enumerate(lines):
+        if "global_load_dword" in ln:
+            loads += 1
+            if any("s_waitcnt vmcnt(0)" in x for x in lines[i + 1:i + 5]):
+                serial += 1
+    assert loads >= 2, (loads, kernel)
+    assert serial <= 2, f"{serial} of {loads} loads waited for at once in {kernel}"
