@@ -6,8 +6,10 @@ Workload (BASELINE.json configs[2], the N = 2^16 configuration the metric is quo
   [1024][8][65536] u64 residue batch (4 GiB) resident in HBM.  Secondary line items:
   inverse NTT and encode+CRT ops/s (RNS decompose + wide CRT compose -> f64) on the same shape.
 
-Multi-GPU: one process per GPU (torchrun), residue-batch sharding -- every rank transforms its own
-batch (weak scaling), no data-path collective; barrier + max-over-ranks timing.
+Multi-GPU: one process per GPU, residue-batch sharding -- every rank transforms its own batch (weak
+scaling), no data-path collective; barrier + max-over-ranks timing.  Under a launcher (torchrun sets
+WORLD_SIZE, which must equal --gpus) this process is one rank; `python bench.py --gpus N` with no
+launcher starts the N ranks itself (launch_ranks) before anything touches the GPU.
 
 Run: python bench.py [--gpus N --steps K --warmup W]
 """
@@ -39,7 +41,6 @@ def parse():
     ap.add_argument("--ntt-wg", type=int, default=None, help="MFHE_OPT_NTT_WG_PER_CU override (tuning)")
     ap.add_argument("--ntt-prefetch", type=int, default=None, help="MFHE_OPT_NTT_PREFETCH override (tuning)")
     ap.add_argument("--ntt-chunk", type=int, default=None, help="MFHE_OPT_NTT_CHUNK_BYTES override (tuning)")
-    ap.add_argument("--ntt-fused", type=int, default=None, help="MFHE_OPT_NTT_FUSED override (tuning)")
     ap.add_argument("--ntt-pack", type=int, default=None, help="MFHE_OPT_NTT_PACK override (tuning)")
     ap.add_argument("--ntt-plan", type=int, default=None, help="MFHE_OPT_NTT_PLAN override (tuning)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
@@ -50,6 +51,7 @@ def parse():
     ap.add_argument("--only", default="all", help="all | ntt | crt | recombine | c4 | c5 (profiling)")
     ap.add_argument("--recombine-batch", type=int, default=256,
                     help="polys per step for the residue-shard INTT + CRT recombine line (0 = skip)")
+    ap.add_argument("--launch-check", action="store_true", help=argparse.SUPPRESS)
     return ap.parse_args()
 
 
@@ -371,6 +373,9 @@ def c5_line(world, rank, barrier, timed, backend, reps=2, recv_gib=2.0):
     N = 1 << log_n
     if L % world or batch % world:
         return {"skipped": f"world {world} does not divide 32 limbs / 4096 polys"}
+    if world > 1 and backend != "nccl":
+        # decided before anything is allocated (the shard is 128/G GiB per rank)
+        return {"skipped": f"world {world}: the C5 recombine needs the RCCL communicator (backend {backend})"}
     moduli = gen_moduli(50, 1 << (log_n + 2), L)
     s0, lg = mdist.limb_range(L, world, rank)
     ctx = mfhe.Context(moduli[s0:s0 + lg], log_n, mfhe.CONV_PHANTOM)   # this rank's limbs: NTT tables
@@ -386,19 +391,43 @@ def c5_line(world, rank, barrier, timed, backend, reps=2, recv_gib=2.0):
         ctx.rns_decompose(z, shard[p0 * lg * N:(p0 + cpg) * lg * N], cpg, N, stream=stream)
     del z
     out = torch.empty(batch // world * N, dtype=torch.float64, device=dev)
-    comm = mfhe.Comm.create() if world > 1 and backend == "nccl" else None
-    modes = ("alltoall", "allgather") if world > 1 else ("local",)
-    # chunk so one exchange receives <= recv_gib: all-to-all receives cp/G polys x 32 limbs, all-gather cp x 32
+    if world > 1:
+        comm = mfhe.Comm.create()
+        modes = ("alltoall", "allgather")
+    else:
+        # N = 1: the local compose, and the same native chunked path over a 1-rank communicator (its "exchange"
+        # is a device copy), which prices the pipeline's own overhead
+        comm = mfhe.Comm.from_id(mfhe.Comm.unique_id(), 1, 0)
+        modes = ("local", "alltoall")
+    # chunk so one receive half holds <= recv_gib / 2 (two halves, exchange k + 1 beside compose k): all-to-all
+    # receives cp/G polys x 32 limbs per chunk, all-gather cp x 32
     per_poly = L * N * 8
-    chunks = {"alltoall": int(recv_gib * 2 ** 30 // per_poly) * world, "allgather": int(recv_gib * 2 ** 30 // per_poly),
-              "local": batch}
-    if comm is not None:
-        for m in modes:
-            ctx_all.crt_recombine_reserve(comm, m, max(world, chunks[m] // world * world), N)
+    half = recv_gib / 2 * 2 ** 30
+    chunks = {"alltoall": int(half // per_poly) * world, "allgather": int(half // per_poly), "local": batch}
+    for m in modes:
+        if m != "local":
+            ctx_all.crt_recombine_chunked_reserve(comm, m, chunks[m], N)
 
     def ntt():
         ctx.ntt_fwd(shard, batch=batch, stream=stream)
         ctx.ntt_inv(shard, batch=batch, stream=stream)
+
+    def check(m):
+        """Every output row against its regenerated message: |err| <= 2^-36 (llround to delta = 2^35, exact
+        CRT).  Row r of this rank holds poly owned_polys(...)[r] (chunk order)."""
+        own = torch.tensor(mdist.owned_polys(batch, world, rank, chunks[m]) if m != "local" else list(range(batch)),
+                           dtype=torch.int64, device=dev)
+        rows = torch.arange(own.numel(), device=dev)
+        g.manual_seed(0x4D46484500000005)
+        zz = torch.empty(cpg * N, dtype=torch.float64, device=dev)
+        err = 0.0
+        for p0 in range(0, batch, cpg):
+            zz.uniform_(-1.0, 1.0, generator=g)
+            sel = (own >= p0) & (own < p0 + cpg)
+            r, p = rows[sel], own[sel] - p0
+            if r.numel():
+                err = max(err, float((out.view(-1, N)[r] - zz.view(-1, N)[p]).abs().nan_to_num(nan=float("inf")).max()))
+        return err
 
     res = {}
     w, _ = timed(ntt, reps, 1)
@@ -412,23 +441,20 @@ def c5_line(world, rank, barrier, timed, backend, reps=2, recv_gib=2.0):
                 ctx_all.crt_compose_f64(shard, out, batch, N, stream=stream)
             else:
                 mdist.crt_recombine_chunked(ctx_all, shard, batch, N, m, chunks[m], out, stream=stream, comm=comm)
-        if comm is None and m != "local":
-            return {"skipped": f"the C5 recombine needs the RCCL communicator (backend {backend})"}
+        out.fill_(float("nan"))
         w, _ = timed(step, reps, 1)
         t = w / reps
         recv = (world - 1) / world * batch * per_poly / (world if m == "alltoall" else 1)
+        err = check(m)
         res[m] = {"ms": round(t * 1e3, 3), "recombine_ms": round((t - t_ntt) * 1e3, 3),
                   "polys_per_s": round(batch / t), "chunk_polys": min(batch, chunks[m]),
                   "recv_GiB_per_gpu": round(recv / 2 ** 30, 2),
-                  "recv_GBps_per_gpu": round(recv / max(t - t_ntt, 1e-9) / 1e9, 1)}
-    # spot check of the last mode run: the first output row of every rank is poly rank * (chunk / G) (poly 0
-    # on rank 0), whose message is regenerated here: |err| <= 2^-36 (llround to delta = 2^35, exact CRT)
-    own0 = mdist.owned_polys(batch, world, rank, chunks[modes[-1]])[0]
-    g.manual_seed(0x4D46484500000005)
-    z = torch.empty(cpg * N, dtype=torch.float64, device=dev).uniform_(-1.0, 1.0, generator=g)
-    torch.cuda.synchronize()
-    res["max_err_first_row"] = float((out[:N] - z[own0 * N:(own0 + 1) * N]).abs().max())
-    res["check_2^-36"] = res["max_err_first_row"] <= 2.0 ** -36
+                  "recv_GBps_per_gpu": round(recv / max(t - t_ntt, 1e-9) / 1e9, 1),
+                  "max_err_all_rows": err, "check_2^-36": err <= 2.0 ** -36}
+        if m != "local":
+            res[m]["path"] = ("mfhe_crt_recombine_chunked: RCCL exchange of chunk k+1 on the communicator's stream "
+                              "beside the compose of chunk k, two receive halves" +
+                              (" (1-rank communicator: the exchange is a device copy)" if world == 1 else ""))
     if comm is not None:
         comm.close()
     ctx.close()
@@ -590,10 +616,72 @@ def u64_line(reps=10):
     return res
 
 
+def free_port() -> int:
+    import socket
+    with socket.socket(socket.AF_INET, socket.SOCK_STREAM) as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def launch_ranks(n: int) -> int:
+    """`bench.py --gpus N` with no launcher around it: start N rank processes (torch.distributed.run, one per
+    GPU, rendezvous on 127.0.0.1) and wait for them.  This parent never touches the GPU (it does not even import
+    torch): it forwards the ranks' output line by line to stderr and re-prints rank 0's one JSON line on stdout,
+    then exits with the ranks' exit status (non-zero also when no JSON line came back)."""
+    import subprocess
+    cmd = [sys.executable, "-u", "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={n}",
+           "--master-addr=127.0.0.1", f"--master-port={free_port()}", str(Path(__file__).resolve()), *sys.argv[1:]]
+    print(f"bench.py: --gpus {n} without WORLD_SIZE -> launching {n} ranks: {' '.join(cmd)}", file=sys.stderr, flush=True)
+    env = dict(os.environ, MFHE_BENCH_LAUNCHED="1")
+    p = subprocess.Popen(cmd, stdout=subprocess.PIPE, text=True, env=env)
+    line = None
+    for ln in p.stdout:
+        s = ln.strip()
+        if s.startswith("{") and '"metric"' in s:
+            try:
+                json.loads(s)
+                line = s
+                continue
+            except ValueError:
+                pass
+        sys.stderr.write(ln)
+        sys.stderr.flush()
+    rc = p.wait()
+    if line is not None:
+        print(line, flush=True)
+    if rc == 0 and line is None:
+        print("bench.py: the ranks exited 0 but printed no JSON line", file=sys.stderr)
+        return 1
+    return rc
+
+
 def main():
     args = parse()
+    env_world = os.environ.get("WORLD_SIZE")
+    if env_world is None and args.gpus > 1:
+        sys.exit(launch_ranks(args.gpus))
+    if env_world is not None and int(env_world) != args.gpus:
+        sys.exit(f"bench.py: WORLD_SIZE={env_world} from the launcher but --gpus {args.gpus}: they must agree "
+                 f"(n_gpus is reported from the ranks that actually run)")
+    if args.gpus < 1:
+        sys.exit("bench.py: --gpus must be >= 1")
     import torch
     import torch.distributed as dist
+
+    if args.launch_check:
+        # CPU rehearsal of the launcher (tests/test_bench_cli.py): the ranks meet over gloo, no GPU
+        w = int(os.environ.get("WORLD_SIZE", "1"))
+        if w > 1:
+            dist.init_process_group("gloo")
+        t = torch.ones(1)
+        if w > 1:
+            dist.all_reduce(t)
+        if int(os.environ.get("RANK", "0")) == 0:
+            print(json.dumps({"metric": "launch-check", "n_gpus": w, "value": t.item(),
+                              "launched_by_bench": os.environ.get("MFHE_BENCH_LAUNCHED") == "1"}), flush=True)
+        if w > 1:
+            dist.destroy_process_group()
+        return
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
@@ -621,7 +709,7 @@ def main():
     if args.arith:
         ctx.set_arith(args.arith)
     for opt, val in ((4, args.ntt_wg), (5, args.ntt_prefetch), (mfhe.OPT_NTT_CHUNK_BYTES, args.ntt_chunk),
-                     (6, args.ntt_fused), (mfhe.OPT_NTT_PACK, args.ntt_pack), (mfhe.OPT_NTT_PLAN, args.ntt_plan)):
+                     (mfhe.OPT_NTT_PACK, args.ntt_pack), (mfhe.OPT_NTT_PLAN, args.ntt_plan)):
         if val is not None:
             ctx.set_option(opt, val)
     stream = torch.cuda.current_stream()
@@ -737,7 +825,9 @@ def main():
             c4comm = mfhe.Comm.create()
         else:
             c4comm = mfhe.Comm.from_id(mfhe.Comm.unique_id(), 1, 0) if world == 1 else None
-        if c4comm is not None:
+        if c4comm is None:
+            c4 = {"skipped": f"world {world}: the C4 decode recombine needs the RCCL communicator (backend {backend})"}
+        else:
             try:
                 c4 = c4_line(world, rank, c4comm, barrier)
             except Exception as e:   # a secondary line must not cost the headline line

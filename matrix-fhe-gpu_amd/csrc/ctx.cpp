@@ -606,7 +606,6 @@ extern "C" int mfhe_ctx_create(const uint64_t* moduli, int L, int log_n, int con
 extern "C" int mfhe_ctx_destroy(mfhe_ctx* c) {
     if (!c) return MFHE_OK;
     if (c->ws) (void)hipFree(c->ws);
-    if (c->fused_buf) (void)hipFree(c->fused_buf);
     if (c->gemm_ws) (void)hipFree(c->gemm_ws);
     if (c->wd_ws) (void)hipFree(c->wd_ws);
     for (void* p : c->allocs) (void)hipFree(p);
@@ -670,18 +669,9 @@ extern "C" int mfhe_ctx_set_option(mfhe_ctx* c, int opt, int64_t v) {
             c->ntt_pack = (int)v;
             return MFHE_OK;
         case MFHE_OPT_NTT_FUSED:
-            if (v < 0 || v > 1) return set_error(MFHE_EINVAL, "fused must be 0 or 1");
-            if (v) {
-                int dev = 0;
-                if (hipGetDevice(&dev) == hipSuccess && dev != c->device)
-                    return set_error(MFHE_EINVAL, "fused: set the option on the context's device");
-                if (int rc = xcc_census(c)) return rc;
-            }
-            c->ntt_fused = (int)v;
-            return MFHE_OK;
-        case MFHE_OPT_NTT_FUSED_LAG:
-            if (v < 1 || v > 64) return set_error(MFHE_EINVAL, "fused lag must be in [1, 64]");
-            c->ntt_fused_lag = (int)v;
+            // the one-launch L2 hand-off NTT was removed in r04 (slower than the two-pass plan, and its hand-off
+            // was never proven): 0 is accepted, anything else is not
+            if (v != 0) return set_error(MFHE_EUNSUPPORTED, "the fused NTT was removed (DESIGN.md §3.1); only 0 is accepted");
             return MFHE_OK;
         case MFHE_OPT_WCRT_MFMA:
             if (v < 0 || v > 3) return set_error(MFHE_EINVAL, "wcrt mfma must be 0, 1, 2 or 3");
@@ -737,25 +727,13 @@ extern "C" int mfhe_ctx_get_option(const mfhe_ctx* c, int opt, int64_t* v) {
         case MFHE_OPT_NTT_PLAN: *v = c->ntt_plan; return MFHE_OK;
         case MFHE_OPT_NTT_WG_PER_CU: *v = c->ntt_wg_per_cu; return MFHE_OK;
         case MFHE_OPT_NTT_PREFETCH: *v = c->ntt_prefetch; return MFHE_OK;
-        case MFHE_OPT_NTT_FUSED: *v = c->ntt_fused; return MFHE_OK;
+        case MFHE_OPT_NTT_FUSED: *v = 0; return MFHE_OK;
         case MFHE_OPT_NTT_PACK: *v = c->ntt_pack; return MFHE_OK;
         case MFHE_OPT_WCRT_PIPE: *v = c->wcrt_pipe; return MFHE_OK;
         case MFHE_OPT_WCRT_MFMA: *v = c->d_wVdig ? c->wcrt_mfma : 0; return MFHE_OK;
         case MFHE_OPT_CGEMM_MFMA: *v = c->cgemm_mfma; return MFHE_OK;
         case MFHE_OPT_HE_FUSED: *v = c->he_fused; return MFHE_OK;
         case MFHE_OPT_TRACE_SPLIT: *v = c->trace_split; return MFHE_OK;
-        case MFHE_OPT_NTT_FUSED_LAG: *v = c->ntt_fused_lag; return MFHE_OK;
-        case MFHE_OPT_NTT_FUSED_ERRORS: {
-            // synchronous: the error word of the last fused launch (0 = no spin timed out)
-            uint32_t e = 0;
-            if (c->fused_buf) {
-                hipError_t he = hipDeviceSynchronize();
-                if (he == hipSuccess) he = hipMemcpy(&e, (const char*)c->fused_buf + 16 * 128 + 4, 4, hipMemcpyDeviceToHost);
-                if (he != hipSuccess) return hip_error(he, "fused error word");
-            }
-            *v = e;
-            return MFHE_OK;
-        }
         case MFHE_OPT_CRT_WORDS: *v = c->W; return MFHE_OK;
         default: return set_error(MFHE_EINVAL, "unknown option");
     }

@@ -75,12 +75,45 @@ struct mfhe_comm {
     ncclComm_t comm = nullptr;
     bool owned = false;
     int nranks = 1, rank = 0, device = 0;
-    void* recv = nullptr;   // receive buffer of the recombine exchange
+    void* recv = nullptr;   // receive buffer of the recombine exchange (the chunked form uses two halves)
     size_t recv_bytes = 0;
-    int32_t* flags = nullptr;   // comm_agree: [nranks] gathered verdicts + [1] this rank's
+    int32_t* flags = nullptr;   // comm_agree: [nranks] gathered verdicts + [1] this rank's (allocated at creation)
+    // chunked recombine: the exchanges run on xs, the composes on the caller's stream.  ev_x[b]: exchange into
+    // receive half b done; ev_c[b]: compose out of half b done (xs waits on it before refilling b, also across
+    // calls); ev_in: the caller's stream reached the call (the shard is ready)
+    hipStream_t xs = nullptr;
+    hipEvent_t ev_in = nullptr, ev_x[2] = {nullptr, nullptr}, ev_c[2] = {nullptr, nullptr};
+    bool c_recorded[2] = {false, false};
 };
 
 using mfhe::set_error;
+
+namespace {
+void comm_free_resources(mfhe_comm* c) {
+    if (c->recv) (void)hipFree(c->recv);
+    if (c->flags) (void)hipFree(c->flags);
+    for (hipEvent_t e : {c->ev_in, c->ev_x[0], c->ev_x[1], c->ev_c[0], c->ev_c[1]})
+        if (e) (void)hipEventDestroy(e);
+    if (c->xs) (void)hipStreamDestroy(c->xs);
+    c->recv = nullptr;
+    c->flags = nullptr;
+    c->xs = nullptr;
+}
+
+// Everything a communicator needs besides RCCL itself, allocated when it is created: a failure here fails the
+// creating call, never a later collective (where one rank returning early would leave its peers blocked).
+int comm_alloc_resources(mfhe_comm* c) {
+    hipError_t he = hipMalloc(&c->flags, (size_t)(c->nranks + 1) * sizeof(int32_t));
+    if (he == hipSuccess) he = hipStreamCreateWithFlags(&c->xs, hipStreamNonBlocking);
+    for (hipEvent_t* e : {&c->ev_in, &c->ev_x[0], &c->ev_x[1], &c->ev_c[0], &c->ev_c[1]})
+        if (he == hipSuccess) he = hipEventCreateWithFlags(e, hipEventDisableTiming);
+    if (he != hipSuccess) {
+        comm_free_resources(c);
+        return mfhe::hip_error(he, "communicator resources (flags, exchange stream, events)");
+    }
+    return MFHE_OK;
+}
+}  // namespace
 
 extern "C" int mfhe_comm_unique_id(uint8_t* id) {
     if (!id) return set_error(MFHE_EINVAL, "null id");
@@ -104,14 +137,21 @@ extern "C" int mfhe_comm_init(const uint8_t* id, int nranks, int rank, mfhe_comm
         delete c;
         return mfhe::hip_error(he, "hipGetDevice");
     }
+    c->nranks = nranks;
+    c->rank = rank;
+    // local resources first: a rank that fails here never enters ncclCommInitRank, so its peers' init fails
+    // by RCCL's own bootstrap timeout instead of a later collective hanging
+    if (int rc = comm_alloc_resources(c)) {
+        delete c;
+        return rc;
+    }
     ncclResult_t e = rccl().CommInitRank(&c->comm, nranks, u, rank);
     if (e != ncclSuccess) {
+        comm_free_resources(c);
         delete c;
         return nccl_error(e, "ncclCommInitRank");
     }
     c->owned = true;
-    c->nranks = nranks;
-    c->rank = rank;
     *out = c;
     return MFHE_OK;
 }
@@ -129,6 +169,10 @@ extern "C" int mfhe_comm_wrap(void* nccl_comm, mfhe_comm** out) {
         return nccl_error(e, "ncclCommCount/UserRank");
     }
     (void)hipGetDevice(&c->device);
+    if (int rc = comm_alloc_resources(c)) {
+        delete c;
+        return rc;
+    }
     *out = c;
     return MFHE_OK;
 }
@@ -136,14 +180,11 @@ extern "C" int mfhe_comm_wrap(void* nccl_comm, mfhe_comm** out) {
 extern "C" int mfhe_comm_destroy(mfhe_comm* c) {
     if (!c) return MFHE_OK;
     int rc = MFHE_OK;
-    if (c->recv) {
-        hipError_t he = hipFree(c->recv);
-        if (he != hipSuccess) rc = mfhe::hip_error(he, "hipFree");
+    if (c->xs) {
+        hipError_t he = hipStreamSynchronize(c->xs);
+        if (he != hipSuccess) rc = mfhe::hip_error(he, "hipStreamSynchronize");
     }
-    if (c->flags) {
-        hipError_t he = hipFree(c->flags);
-        if (he != hipSuccess && !rc) rc = mfhe::hip_error(he, "hipFree");
-    }
+    comm_free_resources(c);
     if (c->owned && c->comm) {
         ncclResult_t e = rccl().CommDestroy(c->comm);
         if (e != ncclSuccess && !rc) rc = nccl_error(e, "ncclCommDestroy");
@@ -181,10 +222,8 @@ int comm_agree(mfhe_comm* c, int local_rc, hipStream_t s) {
     if (c->nranks == 1) return local_rc;
     if (int rc = need_rccl()) return local_rc ? local_rc : rc;
     const std::string mine = local_rc ? mfhe_last_error() : "";
-    if (!c->flags && hipMalloc(&c->flags, (size_t)(c->nranks + 1) * sizeof(int32_t)) != hipSuccess) {
-        c->flags = nullptr;
-        return local_rc ? local_rc : set_error(MFHE_ENOMEM, "comm_agree: hipMalloc failed");
-    }
+    // c->flags exists since the communicator's creation (comm_alloc_resources): nothing here can fail before
+    // this rank has joined the all-gather its peers are waiting in
     std::vector<int32_t> all((size_t)c->nranks, 0);
     const int32_t v = local_rc;
     hipError_t he = hipMemcpyAsync(c->flags + c->nranks, &v, sizeof v, hipMemcpyHostToDevice, s);
@@ -269,4 +308,80 @@ extern "C" int mfhe_crt_recombine_sharded(mfhe_ctx* ctx, mfhe_comm* c, int mode,
     }
     if (e != ncclSuccess) return nccl_error(e, mode == MFHE_XCHG_ALLGATHER ? "ncclAllGather" : "ncclAllToAll");
     return mfhe_crt_compose_f64_sharded(ctx, recv + off, G, stride, bs, ncoeff, d_out, out_stride, s);
+}
+
+namespace {
+// polys per chunk of the chunked recombine: a multiple of G, at least G, at most npoly
+size_t chunk_polys_of(size_t chunk_polys, size_t npoly, int G) {
+    size_t cp = chunk_polys / (size_t)G * (size_t)G;
+    if (cp < (size_t)G) cp = (size_t)G;
+    return cp < npoly ? cp : npoly;
+}
+}  // namespace
+
+extern "C" int mfhe_crt_recombine_chunked_reserve(mfhe_ctx* ctx, mfhe_comm* c, int mode, size_t chunk_polys,
+                                                  size_t ncoeff) {
+    if (!c) return set_error(MFHE_EINVAL, "null comm");
+    const size_t cp = chunk_polys_of(chunk_polys, (size_t)-1, c->nranks);
+    size_t words = 0;
+    if (int rc = xchg_shape(ctx, c, mode, cp, ncoeff, &words)) return rc;
+    return grow(c, 2 * words * sizeof(uint64_t));
+}
+
+// The chunked recombine, pipelined ("chunked all-gather pipelined with compose").  The
+// polynomials go in chunks of cp (a multiple of G); chunk k is one exchange of the chunk's shard rows
+// [p0, p0 + cp) into receive half k % 2, run on the communicator's stream xs, and one in-place sharded compose of
+// this rank's cp / G polys of the chunk out of that half, on the caller's stream s.  Events order them: the
+// compose of chunk k waits for its exchange; the exchange of chunk k + 2 waits for the compose of chunk k (the
+// half it refills).  So the exchange of chunk k + 1 runs while chunk k composes.  Output rows: compact (row
+// k * cp / G + j, the order of mfhe/dist.py owned_polys) or, with MFHE_RECOMBINE_ROWS_GLOBAL, the global
+// polynomial index p0 + rank * cp / G + j (rows of other ranks untouched).  Every chunk's exchange is complete
+// before s proceeds past this call (the last compose waits for the last exchange, and xs runs them in order).
+extern "C" int mfhe_crt_recombine_chunked(mfhe_ctx* ctx, mfhe_comm* c, int mode, const uint64_t* d_shard,
+                                          size_t npoly, size_t ncoeff, size_t chunk_polys, double* d_out,
+                                          size_t out_stride, int flags, mfhe_stream_t s) {
+    size_t words = 0;
+    if (int rc = xchg_shape(ctx, c, mode, npoly, ncoeff, &words)) return rc;   // G | L, G | npoly, mode
+    if (npoly == 0 || ncoeff == 0) return MFHE_OK;
+    if (!d_shard || !d_out || out_stride == 0) return set_error(MFHE_EINVAL, "recombine: bad pointer / stride");
+    if (flags & ~MFHE_RECOMBINE_ROWS_GLOBAL) return set_error(MFHE_EINVAL, "recombine: unknown flags");
+    if (int rc = need_rccl()) return rc;
+    const int G = c->nranks;
+    const size_t lg = (size_t)(ctx->L / G), cp = chunk_polys_of(chunk_polys, npoly, G);
+    size_t cw = 0;
+    if (int rc = xchg_shape(ctx, c, mode, cp, ncoeff, &cw)) return rc;
+    if (int rc = grow(c, 2 * cw * sizeof(uint64_t))) return rc;
+    uint64_t* half[2] = {static_cast<uint64_t*>(c->recv), static_cast<uint64_t*>(c->recv) + cw};
+    const hipStream_t st = (hipStream_t)s;
+    MFHE_HIP(hipEventRecord(c->ev_in, st));
+    MFHE_HIP(hipStreamWaitEvent(c->xs, c->ev_in, 0));
+    size_t k = 0;
+    for (size_t p0 = 0; p0 < npoly; p0 += cp, ++k) {
+        const size_t n = npoly - p0 < cp ? npoly - p0 : cp;   // polys of this chunk (a multiple of G)
+        const size_t bs = n / (size_t)G, shard = n * lg * ncoeff;
+        const int b = (int)(k & 1);
+        if (c->c_recorded[b]) MFHE_HIP(hipStreamWaitEvent(c->xs, c->ev_c[b], 0));
+        const uint64_t* send = d_shard + p0 * lg * ncoeff;
+        ncclResult_t e;
+        size_t off, stride;
+        if (mode == MFHE_XCHG_ALLGATHER) {
+            e = rccl().AllGather(send, half[b], shard, ncclUint64, c->comm, c->xs);
+            off = (size_t)c->rank * bs * lg * ncoeff;
+            stride = shard;
+        } else {
+            e = rccl().AllToAll(send, half[b], bs * lg * ncoeff, ncclUint64, c->comm, c->xs);
+            off = 0;
+            stride = bs * lg * ncoeff;
+        }
+        if (e != ncclSuccess) return nccl_error(e, mode == MFHE_XCHG_ALLGATHER ? "ncclAllGather" : "ncclAllToAll");
+        MFHE_HIP(hipEventRecord(c->ev_x[b], c->xs));
+        MFHE_HIP(hipStreamWaitEvent(st, c->ev_x[b], 0));
+        const size_t row = (flags & MFHE_RECOMBINE_ROWS_GLOBAL) ? p0 + (size_t)c->rank * bs : p0 / (size_t)G;
+        if (int rc = mfhe_crt_compose_f64_sharded(ctx, half[b] + off, G, stride, bs, ncoeff,
+                                                  d_out + row * ncoeff * out_stride, out_stride, s))
+            return rc;
+        MFHE_HIP(hipEventRecord(c->ev_c[b], st));
+        c->c_recorded[b] = true;
+    }
+    return MFHE_OK;
 }

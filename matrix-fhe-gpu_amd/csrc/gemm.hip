@@ -1115,6 +1115,38 @@ __global__ __launch_bounds__(256, D <= 5 ? 2 : 1) void mod_gemm_mfma_ring_kernel
     mfma_epilogue<D, MODE>(a, acc, l, mb + wm, (uint32_t)(pb + wp), r, h, Ppad, icc);
 }
 
+// The ring kernel's waits are counted (vmcnt(D) / vmcnt(2D): the DMAs of the stages still in flight).  A build in
+// which it spills would add scratch traffic to the counted ops; checked once per instantiation from the code
+// object's metadata, and such a build runs the two-stage LDS kernel (vmcnt(0) waits) instead.  AHEAD is D <= 5
+// only: at D = 6 its extra A fragment spills (tests/test_isa.py pins the shipped instantiations' instruction mix).
+template <int D, int MODE, bool AHEAD>
+static bool ring_usable() {
+    static int ok = -1;
+    if (ok < 0) {
+        hipFuncAttributes fa{};
+        ok = hipFuncGetAttributes(&fa, reinterpret_cast<const void*>(mod_gemm_mfma_ring_kernel<D, MODE, AHEAD>)) ==
+                     hipSuccess &&
+             fa.localSizeBytes == 0;
+    }
+    return ok == 1;
+}
+
+// pipe: 1 = two-stage LDS kernel; 3 = ring + one-ahead A read (D <= 5); anything else = ring
+template <int D, int MODE>
+static void launch_staged(int pipe, dim3 grid, hipStream_t s, const ModGemmArgs& f, uint32_t Ppad, int l0) {
+    if constexpr (D <= 5) {
+        if (pipe == 3 && ring_usable<D, MODE, true>()) {
+            hipLaunchKernelGGL((mod_gemm_mfma_ring_kernel<D, MODE, true>), grid, dim3(256), 0, s, f, Ppad, l0);
+            return;
+        }
+    }
+    if (pipe != 1 && ring_usable<D, MODE, false>()) {
+        hipLaunchKernelGGL((mod_gemm_mfma_ring_kernel<D, MODE, false>), grid, dim3(256), 0, s, f, Ppad, l0);
+        return;
+    }
+    hipLaunchKernelGGL((mod_gemm_mfma_lds_kernel<D, MODE>), grid, dim3(256), 0, s, f, Ppad, l0);
+}
+
 size_t mod_gemm_mfma_ws(uint32_t P, int L, int D) {
     const uint64_t Ppad = ((uint64_t)P + 63) / 64 * 64;
     return (size_t)L * D * Ppad * MK + (size_t)L * 2 * Ppad * 8;   // digit planes, then the factored d0
@@ -1169,16 +1201,9 @@ static int launch_factored(const ModGemmArgs& a, int L, hipStream_t s) {
         int l1 = l0 + 1;
         while (l1 < L && (a.limbD ? std::max(a.limbD[l1], 5) : a.D) == d) ++l1;
         const dim3 grid(2 * Ppad / 64, FK / 64, l1 - l0);
-        if (a.pipe == 3) {
-            if (d == 5) hipLaunchKernelGGL((mod_gemm_mfma_ring_kernel<5, 1, true>), grid, dim3(256), 0, s, f, Ppad, l0);
-            else hipLaunchKernelGGL((mod_gemm_mfma_ring_kernel<6, 1, true>), grid, dim3(256), 0, s, f, Ppad, l0);
-        } else if (a.pipe != 1) {   // 0 (auto) and 2: the ring (K = 256: four 64-k stages leave the fill exposed)
-            if (d == 5) hipLaunchKernelGGL((mod_gemm_mfma_ring_kernel<5, 1, false>), grid, dim3(256), 0, s, f, Ppad, l0);
-            else hipLaunchKernelGGL((mod_gemm_mfma_ring_kernel<6, 1, false>), grid, dim3(256), 0, s, f, Ppad, l0);
-        } else {
-            if (d == 5) hipLaunchKernelGGL((mod_gemm_mfma_lds_kernel<5, 1>), grid, dim3(256), 0, s, f, Ppad, l0);
-            else hipLaunchKernelGGL((mod_gemm_mfma_lds_kernel<6, 1>), grid, dim3(256), 0, s, f, Ppad, l0);
-        }
+        // 0 (auto) and 2: the ring (K = 256: four 64-k stages leave the fill exposed)
+        if (d == 5) launch_staged<5, 1>(a.pipe, grid, s, f, Ppad, l0);
+        else launch_staged<6, 1>(a.pipe, grid, s, f, Ppad, l0);
         MFHE_CHECK_LAUNCH("mod_gemm_mfma_lds_kernel (factored)");
         l0 = l1;
     }
@@ -1201,16 +1226,8 @@ static int launch_factored_inv(const ModGemmArgs& a, int L, hipStream_t s) {
         int l1 = l0 + 1;
         while (l1 < L && (a.limbD ? std::max(a.limbD[l1], 5) : a.D) == d) ++l1;
         const dim3 grid(2 * Ppad / 64, FK / 64, l1 - l0);
-        if (a.pipe == 3) {
-            if (d == 5) hipLaunchKernelGGL((mod_gemm_mfma_ring_kernel<5, 2, true>), grid, dim3(256), 0, s, f, Ppad, l0);
-            else hipLaunchKernelGGL((mod_gemm_mfma_ring_kernel<6, 2, true>), grid, dim3(256), 0, s, f, Ppad, l0);
-        } else if (a.pipe != 1) {
-            if (d == 5) hipLaunchKernelGGL((mod_gemm_mfma_ring_kernel<5, 2, false>), grid, dim3(256), 0, s, f, Ppad, l0);
-            else hipLaunchKernelGGL((mod_gemm_mfma_ring_kernel<6, 2, false>), grid, dim3(256), 0, s, f, Ppad, l0);
-        } else {
-            if (d == 5) hipLaunchKernelGGL((mod_gemm_mfma_lds_kernel<5, 2>), grid, dim3(256), 0, s, f, Ppad, l0);
-            else hipLaunchKernelGGL((mod_gemm_mfma_lds_kernel<6, 2>), grid, dim3(256), 0, s, f, Ppad, l0);
-        }
+        if (d == 5) launch_staged<5, 2>(a.pipe, grid, s, f, Ppad, l0);
+        else launch_staged<6, 2>(a.pipe, grid, s, f, Ppad, l0);
         MFHE_CHECK_LAUNCH("mod_gemm_mfma kernel (factored inverse)");
         l0 = l1;
     }
@@ -1254,11 +1271,7 @@ int launch_mod_gemm(const ModGemmArgs& a, int L, hipStream_t s) {
             switch (d) {
 #define MFHE_MFMA_CASE(dd)                                                                                    \
     case dd:                                                                                                  \
-        if (a.lds_stage && a.pipe == 3)                                                                       \
-            hipLaunchKernelGGL((mod_gemm_mfma_ring_kernel<dd, 0, (dd <= 5)>), grid, dim3(256), 0, s, a, Ppad, l0); \
-        else if (a.lds_stage && a.pipe == 2)                                                                  \
-            hipLaunchKernelGGL((mod_gemm_mfma_ring_kernel<dd, 0, false>), grid, dim3(256), 0, s, a, Ppad, l0); \
-        else if (a.lds_stage) hipLaunchKernelGGL((mod_gemm_mfma_lds_kernel<dd, 0>), grid, dim3(256), 0, s, a, Ppad, l0); \
+        if (a.lds_stage) launch_staged<dd, 0>(a.pipe >= 2 ? a.pipe : 1, grid, s, a, Ppad, l0);                  \
         else hipLaunchKernelGGL(mod_gemm_mfma_kernel<dd>, grid, dim3(256), 0, s, a, Ppad, l0);                 \
         break;
                 MFHE_MFMA_CASE(5)

@@ -882,16 +882,26 @@ static int decode_sharded_impl(mfhe_ctx* c, mfhe_ctx* call, mfhe_comm* comm, int
     const Geo2 g = geo(c);
     int G = 1, rank = 0;
     RC(comm_size_rank(comm, &G, &rank));
-    uint64_t* coeff = pb->get<uint64_t>(g.words);
+    uint64_t* coeff_re = pb->get<uint64_t>(g.words);
+    uint64_t* coeff_im = pb->get<uint64_t>(g.words);
     double2* ccx = pb->get<double2>(g.cnt);
     double2* ecx = pb->get<double2>(g.cnt);
-    const size_t bs = 512 / G;
-    double2* mine = ccx + (size_t)rank * bs * g.n2;
-    RC(wcrt_gemm(c, c->d_wVinv, ev_re, true, coeff, WOut::Matrix, false, s));
-    RC(mfhe_crt_recombine_sharded(call, comm, mode, coeff, 512, g.n2, (double*)mine, 2, (mfhe_stream_t)s));
-    RC(wcrt_gemm(c, c->d_wVinv, ev_im, true, coeff, WOut::Matrix, false, s));
-    RC(mfhe_crt_recombine_sharded(call, comm, mode, coeff, 512, g.n2, (double*)mine + 1, 2, (mfhe_stream_t)s));
-    RC(comm_allgather_bytes(comm, mine, ccx, bs * g.n2 * sizeof(double2), s));   // in place
+    // both W-INTTs first, then the two chunked recombines back to back: the exchange stream runs the re and im
+    // chunks without a gap while this stream composes (dist.cpp mfhe_crt_recombine_chunked).  Rows land at their
+    // lane index (MFHE_RECOMBINE_ROWS_GLOBAL), so each chunk's lanes [p0, p0 + cp) are [rank][cp / G] in lane order
+    // and one in-place all-gather per chunk completes them on every rank.
+    const size_t cp = mfhe_ctx::PHI / 4 >= (size_t)G ? mfhe_ctx::PHI / 4 / G * G : (size_t)G;
+    RC(wcrt_gemm(c, c->d_wVinv, ev_re, true, coeff_re, WOut::Matrix, false, s));
+    RC(wcrt_gemm(c, c->d_wVinv, ev_im, true, coeff_im, WOut::Matrix, false, s));
+    RC(mfhe_crt_recombine_chunked(call, comm, mode, coeff_re, 512, g.n2, cp, (double*)ccx, 2,
+                                  MFHE_RECOMBINE_ROWS_GLOBAL, (mfhe_stream_t)s));
+    RC(mfhe_crt_recombine_chunked(call, comm, mode, coeff_im, 512, g.n2, cp, (double*)ccx + 1, 2,
+                                  MFHE_RECOMBINE_ROWS_GLOBAL, (mfhe_stream_t)s));
+    for (size_t p0 = 0; p0 < 512; p0 += cp) {
+        const size_t bs = (512 - p0 < cp ? 512 - p0 : cp) / (size_t)G;
+        RC(comm_allgather_bytes(comm, ccx + (p0 + (size_t)rank * bs) * g.n2, ccx + p0 * g.n2,
+                                bs * g.n2 * sizeof(double2), s));   // in place
+    }
     RC(wdft(c, c->d_wdV, ccx, ecx, s));
     RC(xy3(c, c->d_encV, ecx, c->d_encVT, ccx, (double2*)msg, 512, s));
     return MFHE_OK;

@@ -27,7 +27,6 @@ int comm_size_rank(const mfhe_comm* comm, int* size, int* rank);
 int comm_agree(mfhe_comm* comm, int local_rc, hipStream_t s);
 int hip_error(hipError_t e, const char* what);
 int ensure_xy(mfhe_ctx* c);   // XY encoder matrices, built on first use (ctx.cpp)
-int xcc_census(mfhe_ctx* c);  // fused NTT: XCC id -> queue map (ntt.hip), run when MFHE_OPT_NTT_FUSED is set
 
 #define MFHE_HIP(call)                                          \
     do {                                                        \
@@ -85,11 +84,6 @@ struct mfhe_ctx {
     // 2 (default) = FP64 forward column pass with the next tile's LDS-DMA in flight (ntt_coldb.hpp, +0.5% C3, r02)
     int ntt_prefetch = 2;
     int num_cus = 256;
-    int ntt_fused = 0;       // N = 2^15..2^17: both passes in one launch (MFHE_OPT_NTT_FUSED)
-    int ntt_fused_lag = 2;   // pass-2 lag in polynomials per XCD queue
-    void* fused_buf = nullptr;   // FusedSync + arrival arrays, grown on demand
-    int xcc_nq = 0;              // fused NTT: XCDs found by the census (0 = not run yet)
-    uint8_t xcc_qmap[16] = {};   // XCC id -> fused queue index
     int8_t* d_wVdig = nullptr;   // [L][wD][512][512] balanced base-256 digits of V   (i8 MFMA W-CRT)
     int8_t* d_wVidig = nullptr;  // same for V^-1
     uint64_t* d_wrtab = nullptr; // [L][2 wD - 1][2] (256^s mod q, Shoup)
@@ -111,7 +105,6 @@ struct mfhe_ctx {
     int limbs_total = 0;         // residue shard: L of the whole parameter set (0 = this context's L)
     void* gemm_ws = nullptr;     // B digit planes for the MFMA GEMM, grown on demand
     size_t gemm_ws_bytes = 0;
-    size_t fused_bytes = 0;
 
     mfhe::LimbConst* d_limbs = nullptr;  // [L]
     uint64_t* d_dmod = nullptr;          // [L][3] phantom DModulus {value, const_ratio[2]}

@@ -71,7 +71,7 @@ __device__ __forceinline__ void lds_barrier() { asm volatile("s_waitcnt lgkmcnt(
 // One column tile whose DMA has landed in buf ([256 rows][NG] row-major): stages 0..7, the exchange in buf itself,
 // then the raw intermediate (F64: centred doubles; U64: [0, 2q)) stored to base (plain stores, R per thread).
 // tw0: tw[1..15] of the limb (shared), tw1: this thread's round-1 twiddles ((16 + tau) << e) + j.  TW0 / TW1:
-// anything indexable by [0, 15) giving A::Tw -- register arrays (F64), LDS table views (U64, fused kernel).
+// anything indexable by [0, 15) giving A::Tw -- register arrays (F64), LDS table views (U64).
 template <class A, class TW0, class TW1>
 __device__ __forceinline__ void coldb_tile(uint64_t* buf, uint32_t gl, uint32_t tau, const LimbConst& lc,
                                            const TW0& tw0, const TW1& tw1, uint64_t* base, uint32_t off0, int logS) {

@@ -160,7 +160,7 @@ __device__ __forceinline__ TileLoc tile_loc(uint64_t* data, uint64_t batch, int 
 
 // One pass of the transform: LOG_G stages on groups of G = 2^LOG_G elements, one tile (NG groups) per
 // workgroup at a time.  Split into locate / load / compute+store so the persistent pass kernel can
-// prefetch and the fused kernel can run two different passes in one launch.
+// prefetch.
 // PACK (N = 2^16 two-pass plan, FP64 arithmetic, forward): the intermediate between the passes is stored as
 // 50-bit canonical residues instead of 64-bit words.  Unit (rb, t) = the 16 x 16 block of rows 16 rb.. and
 // columns 16 t.., column-major: LO[c][i] u32 (1024 B), MID[c][i] u16 (512 B), TOP[c] 16 x 2 bits (64 B),
@@ -250,20 +250,6 @@ struct NttPass {
             }
         }
     }
-
-    // Loads with an explicit cache policy (CPol aux bits) off the workgroup-uniform tile base (UNI plans):
-    // SGPR buffer descriptor + 32-bit lane offset.  The fused kernel reads the intermediate with sc1
-    // (L1 bypass, served by the XCD's L2: data another CU of this XCD just stored).
-    template <int CPOL>
-    __device__ __forceinline__ void load_pol(const TileLoc& L, uint64_t (&raw)[R]) const {
-        static_assert(UNI, "load_pol needs a workgroup-uniform tile base");
-        const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(L.base, 0, 0x7FFFFFFF, 0x00020000);
-#pragma unroll
-        for (int k = 0; k < R; ++k)
-            raw[k] = __builtin_bit_cast(uint64_t, __builtin_amdgcn_raw_buffer_load_b64(
-                                                      rs, (int)(jidx(L, Gm::g_of(r_load, tau, k)) * 8u), 0, CPOL));
-    }
-    __device__ __forceinline__ void load_l2(const TileLoc& L, uint64_t (&raw)[R]) const { load_pol<16>(L, raw); }
 
     __device__ __forceinline__ void compute_store(const TileLoc& L, const uint64_t (&raw)[R], uint64_t* lds) const {
         uint64_t* my_lds = lds + (size_t)gl * GS;

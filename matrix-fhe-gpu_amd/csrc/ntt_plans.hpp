@@ -1,4 +1,4 @@
-// ntt_plans.hpp -- NTT launch plans (single pass / two-pass / fused) shared by the per-arithmetic,
+// ntt_plans.hpp -- NTT launch plans (single pass / two-pass) shared by the per-arithmetic,
 // per-direction translation units ntt_{f64,u64}_{fwd,inv}.hip (split so they compile in parallel).
 //
 // Plans (one launch per pass over the whole batch; the reference launches
@@ -13,7 +13,6 @@
 
 #include "mfhe_ctx.hpp"
 #include "ntt_coldb.hpp"
-#include "ntt_fused.hpp"
 
 // Groups (contiguous rows) per block-pass workgroup.  N = 2^16: 4 rows (64 threads, 8.7 KiB LDS) rather than 16
 // (256 threads, 34.9 KiB): the block pass gains from residency and 16-row tiles are LDS-bound at 4 per CU;
@@ -62,7 +61,7 @@ struct NttJob {
     int prefetch;         // MFHE_OPT_NTT_PREFETCH
     int pack = 0;         // MFHE_OPT_NTT_PACK: 50-bit packed intermediate (N = 2^16, F64)
     int num_cus;
-    mfhe_ctx* ctx;        // owner of the fused sync buffer (null: raw phantom entry, no fused path)
+    mfhe_ctx* ctx;        // owning context (null: raw phantom entry)
 };
 
 template <class A, class TS, int LOG_G, int LOG_R, int NG, bool COLS, bool INV, bool IN_RAW, bool OUT_RAW, bool TWIST,
@@ -258,74 +257,6 @@ static int two_pass(const NttJob<TS>& j, hipStream_t st) {
     return MFHE_OK;
 }
 
-// Both passes in one launch (ntt_fused.hpp).  Pass 1 / pass 2 are the column / block passes of
-// two_pass (forward) or block / column (inverse), with the same template choices.
-template <class A, class TS, int LOG_GA, int NGA, int LOG_GB, int NGB, bool INV>
-static int fused(const NttJob<TS>& j, hipStream_t st) {
-    using PA = NttPass<A, TS, LOG_GA, 4, NGA, true, INV, INV, !INV, false, false, true>;
-    using PB = NttPass<A, TS, LOG_GB, 4, NGB, false, INV, !INV, INV, false, false, true>;
-    using P1 = std::conditional_t<INV, PB, PA>;
-    using P2 = std::conditional_t<INV, PA, PB>;
-    const uint64_t npl = j.batch * (uint64_t)j.nl;
-    const uint32_t K = (uint32_t)((1ull << (j.logN - LOG_GA)) / NGA);
-    if ((1ull << (j.logN - LOG_GB)) / NGB != K) return set_error(MFHE_EINVAL, "fused NTT: pass tile counts differ");
-    if (npl * K >= 0xFFFFFFFFull) return set_error(MFHE_EINVAL, "NTT batch too large for one fused launch");
-    auto kern = ntt_fused_kernel<P1, P2, TS>;
-    constexpr size_t lds = (P1::LDS_BYTES > P2::LDS_BYTES ? P1::LDS_BYTES : P2::LDS_BYTES) + 16;
-    static int occ = 0;
-    if (occ == 0) {
-        int o = 0;
-        if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&o, kern, P1::NT, lds) != hipSuccess || o < 1) o = 1;
-        occ = o;
-    }
-    const int per_cu = (j.wg_per_cu > 0 && j.wg_per_cu < 16) ? std::min(j.wg_per_cu, occ) : occ;
-    const uint32_t grid = (uint32_t)std::max(8, per_cu * j.num_cus);
-    mfhe_ctx* c = j.ctx;
-    // the XCC census runs when the option is set (mfhe_ctx_set_option, xcc_census), never inside a call that
-    // may be under stream capture
-    if (c->xcc_nq == 0) return set_error(MFHE_ENOTREADY, "fused NTT: XCC census missing (set MFHE_OPT_NTT_FUSED)");
-    const uint32_t nq = (uint32_t)c->xcc_nq;
-    const uint32_t lag = (uint32_t)c->ntt_fused_lag;
-    const uint64_t cap = (npl + nq - 1) / nq + 1;
-    const size_t need = sizeof(FusedSync) + (size_t)kFusedXcc * cap * sizeof(uint32_t);
-    if (c->fused_bytes < need) {
-        if (c->fused_buf) MFHE_HIP(hipFree(c->fused_buf));
-        c->fused_buf = nullptr;
-        c->fused_bytes = 0;
-        MFHE_HIP(hipMalloc(&c->fused_buf, need));
-        c->fused_bytes = need;
-    }
-    MFHE_HIP(hipMemsetAsync(c->fused_buf, 0, need, st));
-    FusedArgs<TS> f;
-    {
-        PassArgs<TS>& a = f.p;
-        a.data = j.data;
-        a.tw = j.tw;
-        a.twist = j.twist;
-        a.ninv = j.ninv;
-        a.limbs = j.limbs;
-        a.qraw = j.qraw;
-        a.qstride = j.qstride;
-        a.batch = j.batch;
-        a.nl = j.nl;
-        a.start_limb = j.start_limb;
-        a.logN = j.logN;
-        a.s0 = 0;   // unused: NttPass derives s0 from the pass kind
-        a.nblocks = (uint32_t)(npl * K);
-    }
-    f.sync = (FusedSync*)c->fused_buf;
-    f.arr = (uint32_t*)((char*)c->fused_buf + sizeof(FusedSync));
-    f.cap = (uint32_t)cap;
-    f.K = K;
-    f.npl = (uint32_t)npl;
-    f.lag = lag;
-    f.nq = nq;
-    for (int x = 0; x < kFusedXcc; ++x) f.qmap[x] = c->xcc_qmap[x];
-    hipLaunchKernelGGL(kern, dim3(grid), dim3(P1::NT), lds, st, f);
-    MFHE_CHECK_LAUNCH("ntt_fused_kernel launch");
-    return MFHE_OK;
-}
-
 template <class A, class TS, bool INV>
 static int run_phantom(const NttJob<TS>& j, hipStream_t st) {
     // auto: N = 2^14 runs two passes (7 + 7, 8-row block tiles): at C2 +1% forward, +7% inverse over the single
@@ -333,13 +264,6 @@ static int run_phantom(const NttJob<TS>& j, hipStream_t st) {
     // (profiles/r02_c2_plans2.txt)
     const bool two = j.logN > 14 || (j.plan == 2 && j.logN >= 12) || (j.plan == 0 && j.logN == 14);
     if (!two) return run_single<A, TS, INV, false>(j, st);
-    if (j.ctx && j.ctx->ntt_fused && j.logN >= 15) {
-        switch (j.logN) {
-            case 15: return fused<A, TS, 8, 16, 7, 32, INV>(j, st);
-            case 16: return fused<A, TS, 8, 16, 8, 16, INV>(j, st);
-            case 17: return fused<A, TS, 9, 8, 8, 16, INV>(j, st);
-        }
-    }
     switch (j.logN) {
         case 12: return two_pass<A, TS, 6, 64, 6, 64, INV>(j, st);
         case 13: return two_pass<A, TS, 7, 32, 6, 64, INV>(j, st);

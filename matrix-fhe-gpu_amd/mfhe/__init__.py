@@ -24,9 +24,10 @@ OK, EINVAL, EUNSUPPORTED, EHIP, ENOMEM, ENOTREADY = 0, 1, 2, 3, 4, 5
 CONV_PHANTOM, CONV_GL, CONV_WCRT = 1, 2, 4
 ARITH_AUTO, ARITH_F64, ARITH_U64 = 0, 1, 2
 OPT_NTT_CHUNK_BYTES, OPT_NTT_PLAN, OPT_CRT_WORDS, OPT_NTT_WG_PER_CU, OPT_NTT_PREFETCH = 1, 2, 3, 4, 5
-OPT_NTT_FUSED, OPT_NTT_FUSED_LAG, OPT_NTT_FUSED_ERRORS, OPT_WCRT_MFMA = 6, 7, 8, 9
+OPT_NTT_FUSED, OPT_WCRT_MFMA = 6, 9   # OPT_NTT_FUSED: removed in r04, only 0 accepted
 OPT_CGEMM_MFMA, OPT_HE_FUSED, OPT_TRACE_SPLIT = 10, 11, 12
 XCHG_ALLGATHER, XCHG_ALLTOALL = 0, 1
+RECOMBINE_ROWS_GLOBAL = 1
 OPT_NTT_PACK = 13
 OPT_WCRT_PIPE = 14
 COMM_ID_BYTES = 128
@@ -127,6 +128,8 @@ _sig("mfhe_comm_info", [_vp, ctypes.POINTER(ctypes.c_int), ctypes.POINTER(ctypes
 _sig("mfhe_allgather_limbs", [_vp, _vp, _sz, _vp, _vp])
 _sig("mfhe_crt_recombine_sharded", [_vp, _vp, ctypes.c_int, _vp, _sz, _sz, _vp, _sz, _vp])
 _sig("mfhe_crt_recombine_reserve", [_vp, _vp, ctypes.c_int, _sz, _sz])
+_sig("mfhe_crt_recombine_chunked", [_vp, _vp, ctypes.c_int, _vp, _sz, _sz, _sz, _vp, _sz, ctypes.c_int, _vp])
+_sig("mfhe_crt_recombine_chunked_reserve", [_vp, _vp, ctypes.c_int, _sz, _sz])
 _sig("mfhe_ctx_set_limb_shard", [_vp, ctypes.c_int, ctypes.c_int])
 _sig("mfhe_decode_sharded", [_vp, _vp, _vp, ctypes.c_int, _vp, _vp, _vp, _vp])
 _sig("mfhe_decrypt_and_decode_sharded", [_vp, _vp, _vp, ctypes.c_int, _vp, _vp, _vp, _vp, _vp])
@@ -402,6 +405,27 @@ class Context:
     def crt_recombine_reserve(self, comm: "Comm", mode, npoly, ncoeff):
         m = _XCHG[mode] if isinstance(mode, str) else mode
         check(lib.mfhe_crt_recombine_reserve(self._h, comm._h, m, npoly, ncoeff), "crt_recombine_reserve")
+
+    def crt_recombine_chunked(self, comm: "Comm", mode, shard, npoly, ncoeff, chunk_polys, out, out_stride=1,
+                              rows_global=False, stream=None):
+        """Chunked, pipelined RCCL recombine (include/mfhe.h mfhe_crt_recombine_chunked): exchange of chunk k + 1
+        on the communicator's stream beside the compose of chunk k on `stream`.  out rows: owned_polys order
+        (npoly/G rows), or the global poly index with rows_global (npoly rows, only this rank's written)."""
+        m = _XCHG[mode] if isinstance(mode, str) else mode
+        g = comm.size
+        lg = self.info().num_limbs // g if g else 0
+        _need(shard, npoly * lg * ncoeff, "shard")
+        rows = npoly if rows_global else (npoly // g if g else 0)
+        _need_strided(out, rows * ncoeff, out_stride, "out")
+        check(lib.mfhe_crt_recombine_chunked(self._h, comm._h, m, _ptr(shard), npoly, ncoeff, chunk_polys, _ptr(out),
+                                             out_stride, RECOMBINE_ROWS_GLOBAL if rows_global else 0,
+                                             _stream_ptr(stream)), "crt_recombine_chunked")
+        return out
+
+    def crt_recombine_chunked_reserve(self, comm: "Comm", mode, chunk_polys, ncoeff):
+        m = _XCHG[mode] if isinstance(mode, str) else mode
+        check(lib.mfhe_crt_recombine_chunked_reserve(self._h, comm._h, m, chunk_polys, ncoeff),
+              "crt_recombine_chunked_reserve")
 
     # ---- W axis / encoder / pipelines (reference geometry, CONV_WCRT) ----
     def _call(self, name, *ptrs, stream=None):

@@ -81,15 +81,40 @@ def owned_polys(batch: int, world: int, rank: int, chunk_polys: int) -> list[int
 
 
 def crt_recombine_chunked(ctx, shard: torch.Tensor, batch: int, ncoeff: int, mode: str, chunk_polys: int,
-                          out: torch.Tensor, group=None, stream=None, comm=None) -> torch.Tensor:
-    """crt_recombine over chunk_plan's poly chunks: shard [batch][Lg][ncoeff] -> out [batch/world][ncoeff] f64,
-    rows in owned_polys order.  Each chunk is one exchange + in-place sharded compose."""
-    world = comm.size if comm is not None else dist.get_world_size(group)
+                          out: torch.Tensor, group=None, stream=None, comm=None, rows_global: bool = False) -> torch.Tensor:
+    """crt_recombine over chunk_plan's poly chunks: shard [batch][Lg][ncoeff] -> out f64, rows in owned_polys
+    order ([batch/world][ncoeff]) or, with rows_global, at the global poly index ([batch][ncoeff], only this
+    rank's rows written).  Each chunk is one exchange + in-place sharded compose.  With `comm` the whole loop is
+    the native pipelined call (mfhe_crt_recombine_chunked: chunk k + 1's RCCL exchange on the communicator's
+    stream beside chunk k's compose); without it, the torch.distributed restatement below, chunk after chunk,
+    which the gloo tests use to pin the same row order."""
+    if comm is not None:
+        return ctx.crt_recombine_chunked(comm, mode, shard, batch, ncoeff, chunk_polys, out, stream=stream,
+                                         rows_global=rows_global)
+    world = dist.get_world_size(group)
+    rank = dist.get_rank(group)
     lg = ctx.info().num_limbs // world
     for p0, cp, row0 in chunk_plan(batch, world, chunk_polys):
         sh = shard[p0 * lg * ncoeff:(p0 + cp) * lg * ncoeff]
-        o = out[row0 * ncoeff:(row0 + cp // world) * ncoeff]
+        r = p0 + rank * (cp // world) if rows_global else row0
+        o = out[r * ncoeff:(r + cp // world) * ncoeff]
         crt_recombine(ctx, sh, cp, ncoeff, mode, group, out=o, stream=stream, comm=comm)
+    return out
+
+
+def decode_recombine(ctx, shard: torch.Tensor, lanes: int, ncoeff: int, mode: str, chunk_polys: int,
+                     out: torch.Tensor, group=None) -> torch.Tensor:
+    """The recombine step of mfhe_decode_sharded (he.hip decode_sharded_impl), restated over torch.distributed:
+    the chunked recombine with rows at their lane index, then one in-place all-gather per chunk, after which
+    every rank holds all `lanes` rows [lanes][ncoeff] in lane order (chunk k's lanes are [rank][cp / G])."""
+    world = dist.get_world_size(group)
+    rank = dist.get_rank(group)
+    crt_recombine_chunked(ctx, shard, lanes, ncoeff, mode, chunk_polys, out, group=group, rows_global=True)
+    for p0, cp, _ in chunk_plan(lanes, world, chunk_polys):
+        bs = cp // world
+        parts = list(out[p0 * ncoeff:(p0 + cp) * ncoeff].view(world, bs * ncoeff).unbind(0))
+        mine = parts[rank].clone()
+        dist.all_gather(parts, mine, group=group)
     return out
 
 

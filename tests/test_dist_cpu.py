@@ -87,8 +87,9 @@ def test_limb_range_rejects_uneven():
 
 
 def _c4_rank(rank, world, port, mode, q):
-    """BASELINE C4 decode exchange: 16 limbs over `world` ranks, every rank composes its lane slice and an
-    all-gather of the f64 slices gives every rank the whole batch (mfhe_decode_sharded's data flow)."""
+    """BASELINE C4 decode exchange: 16 limbs over `world` ranks, the chunked recombine writes every rank's lanes of
+    each chunk at their lane index and one in-place all-gather per chunk gives every rank the whole batch
+    (mfhe_decode_sharded's data flow, he.hip decode_sharded_impl, restated by mfhe.dist.decode_recombine)."""
     import sys
     from pathlib import Path
     root = Path(__file__).resolve().parent.parent
@@ -101,23 +102,18 @@ def _c4_rank(rank, world, port, mode, q):
     dist.init_process_group("gloo", rank=rank, world_size=world)
     try:
         moduli = O.gen_primes(35, 197376, 16)
-        lanes, n2 = 8, 16
+        lanes, n2 = 16, 8
         rng = np.random.default_rng(5)
         v = rng.integers(-(1 << 40), 1 << 40, (lanes, n2))
         full = np.stack([(v.astype(object) % m).astype(np.uint64) for m in moduli], axis=1)   # [lanes][16][n2]
         s0, lg = mdist.limb_range(16, world, rank)
-        shard = torch.from_numpy(full[:, s0:s0 + lg, :].astype(np.int64).copy())
-        buf, off, stride, bs = mdist.exchange_residues(shard, lanes, lg, n2, mode)
-        b = buf.numpy().view(np.uint64)
-        view = np.stack([b[off + s * stride: off + s * stride + bs * lg * n2].reshape(bs, lg, n2)
-                         for s in range(world)], axis=1).reshape(bs, 16, n2)
-        W = O.crt_words(moduli)
-        mag, neg = O.crt_compose(view.ravel(), bs, 16, n2, moduli, W)
-        mine = torch.from_numpy(O.big_to_f64(mag, neg, W, 2.0 ** 35))
-        slices = [torch.empty_like(mine) for _ in range(world)]
-        dist.all_gather(slices, mine)
-        got = torch.cat(slices).numpy()
-        q.put((rank, bool(np.array_equal(got, v.ravel().astype(np.float64) / 2.0 ** 35))))
+        shard = torch.from_numpy(full[:, s0:s0 + lg, :].astype(np.int64).copy()).view(-1)
+        ok = True
+        for chunk in (lanes // 4, lanes, 3 * world):   # 4 chunks (as the decode), one chunk, a ragged last chunk
+            out = torch.full((lanes * n2,), np.nan, dtype=torch.float64)
+            mdist.decode_recombine(_OracleShardCtx(moduli, 2.0 ** 35), shard, lanes, n2, mode, chunk, out)
+            ok = ok and np.array_equal(out.numpy(), v.ravel().astype(np.float64) / 2.0 ** 35)
+        q.put((rank, bool(ok)))
     finally:
         dist.destroy_process_group()
 

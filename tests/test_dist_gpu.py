@@ -91,3 +91,58 @@ def test_sharded_compose_layout_of_g_rank_exchange(mfhe, orc, G, mode):
         torch.cuda.synchronize()
         assert torch.equal(out, ref[g * bs * n:(g + 1) * bs * n])
     ctx.close()
+
+
+@pytest.mark.parametrize("mode", ["allgather", "alltoall"])
+@pytest.mark.parametrize("rows_global", [False, True])
+def test_chunked_recombine_one_rank_equals_unsharded(mfhe, orc, mode, rows_global):
+    """mfhe_crt_recombine_chunked: several chunks, a ragged last chunk (11 polys in chunks of
+    4: 4 + 4 + 3), the exchange on the communicator's stream beside the compose -- bit-identical to the unsharded
+    compose.  Called twice back to back (the second call's first exchanges wait on the first call's composes of
+    the same receive halves), and once more with a chunk as large as the batch."""
+    import torch
+    moduli = orc.gen_primes(50, 1 << 18, 8)
+    ctx = mfhe.Context(moduli, 16)
+    npoly, ncoeff = 11, 1 << 12
+    rng = np.random.default_rng(5)
+    res, v = _residues(rng, npoly, moduli, ncoeff, ctx.info().delta)
+    d = mfhe.to_device_u64(res.ravel())
+    ref = torch.empty(npoly * ncoeff, dtype=torch.float64, device="cuda")
+    ctx.crt_compose_f64(d, ref, npoly, ncoeff)
+    comm = mfhe.Comm.from_id(mfhe.Comm.unique_id(), 1, 0)
+    try:
+        ctx.crt_recombine_chunked_reserve(comm, mode, 4, ncoeff)
+        for chunk in (4, 4, 64, 1):
+            out = torch.full((npoly * ncoeff,), float("nan"), dtype=torch.float64, device="cuda")
+            ctx.crt_recombine_chunked(comm, mode, d, npoly, ncoeff, chunk, out, rows_global=rows_global)
+            torch.cuda.synchronize()
+            assert torch.equal(out, ref), chunk
+        # strided output (the decode writes re / im interleaved)
+        out2 = torch.full((2 * npoly * ncoeff,), float("nan"), dtype=torch.float64, device="cuda")
+        ctx.crt_recombine_chunked(comm, mode, d, npoly, ncoeff, 3, out2[1:], out_stride=2, rows_global=rows_global)
+        torch.cuda.synchronize()
+        assert torch.equal(out2[1::2], ref) and torch.isnan(out2[0::2]).all()
+        np.testing.assert_array_equal(ref.cpu().numpy(), v.ravel().astype(np.float64) / ctx.info().delta)
+    finally:
+        comm.close()
+        ctx.close()
+
+
+def test_chunked_recombine_rejects_bad_arguments(mfhe, orc):
+    import torch
+    moduli = orc.gen_primes(50, 1 << 14, 3)
+    ctx = mfhe.Context(moduli, 12)
+    comm = mfhe.Comm.from_id(mfhe.Comm.unique_id(), 1, 0)
+    try:
+        d = torch.zeros(4 * 3 * 16, dtype=torch.int64, device="cuda")
+        out = torch.zeros(4 * 16, dtype=torch.float64, device="cuda")
+        with pytest.raises(mfhe.MfheError):
+            ctx.crt_recombine_chunked(comm, 7, d, 4, 16, 2, out)
+        with pytest.raises(mfhe.MfheError):   # unknown flag bits
+            mfhe.check(mfhe.lib.mfhe_crt_recombine_chunked(ctx.handle, comm._h, 0, d.data_ptr(), 4, 16, 2,
+                                                           out.data_ptr(), 1, 6, None))
+        with pytest.raises(ValueError):   # undersized output caught on the host
+            ctx.crt_recombine_chunked(comm, "alltoall", d, 4, 16, 2, out[:10])
+    finally:
+        comm.close()
+        ctx.close()

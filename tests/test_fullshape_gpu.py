@@ -2,8 +2,8 @@
 
 BASELINE.json configs exercised at exactly the shape they name (tests/golden/fullshape.py):
   C2        N = 2^14, L = 4, batch 256: forward + inverse NTT
-  C3        N = 2^16, L = 8, batch 1024: forward + inverse NTT (F64 and U64 arithmetic, two-pass and
-            fused plans), 60-bit primes (U64), and the encode -> NTT -> INTT -> decode-with-CRT chain
+  C3        N = 2^16, L = 8, batch 1024: forward + inverse NTT (F64 and U64 arithmetic, DMA and plain
+            column passes), 60-bit primes (U64), and the encode -> NTT -> INTT -> decode-with-CRT chain
             (RNS decompose, forward NTT, inverse NTT, wide CRT compose -> f64) plus the full-path
             integer CRT compose of uniform residues
   C5 shard  N = 2^17, 32 moduli, batch 4096, limbs 4..7 (one GPU's residue shard of 8)
@@ -23,9 +23,6 @@ sys.path.insert(0, str(Path(__file__).resolve().parent / "golden"))
 import fullshape as F  # noqa: E402
 
 pytestmark = pytest.mark.gpu
-
-OPT_FUSED = 6
-
 
 @pytest.fixture(scope="module")
 def dig():
@@ -64,7 +61,7 @@ def _check(got, want, what):
                         f"vs {F.top_digest(want)})"
 
 
-def _run_ntt_config(mfhe, orc, dig, name, arith=0, fused=0, prefetch=None, lag=None):
+def _run_ntt_config(mfhe, orc, dig, name, arith=0, prefetch=None):
     import torch
     cfg = F.NTT_CONFIGS[name]
     N = 1 << cfg["log_n"]
@@ -73,10 +70,6 @@ def _run_ntt_config(mfhe, orc, dig, name, arith=0, fused=0, prefetch=None, lag=N
     ctx = mfhe.Context(allm, cfg["log_n"])
     if arith:
         ctx.set_arith(arith)
-    if fused:
-        ctx.set_option(OPT_FUSED, fused)
-    if lag is not None:
-        ctx.set_option(mfhe.OPT_NTT_FUSED_LAG, lag)
     if prefetch is not None:   # default 2: the DMA column pass; 0: the plain column pass
         ctx.set_option(mfhe.OPT_NTT_PREFETCH, prefetch)
     B, nl, st = cfg["batch"], cfg["nl"], cfg["start"]
@@ -100,10 +93,10 @@ def test_c2_full_shape(mfhe, orc, dig):
     _run_ntt_config(mfhe, orc, dig, "c2")
 
 
-@pytest.mark.parametrize("arith,fused,prefetch", [(0, 0, None), (2, 0, None), (0, 1, None), (0, 0, 0), (2, 0, 0)],
-                         ids=["f64", "u64", "f64-fused", "f64-plain-colpass", "u64-plain-colpass"])
-def test_c3_full_shape(mfhe, orc, dig, arith, fused, prefetch):
-    _run_ntt_config(mfhe, orc, dig, "c3", arith, fused, prefetch)
+@pytest.mark.parametrize("arith,prefetch", [(0, None), (2, None), (0, 0), (2, 0)],
+                         ids=["f64", "u64", "f64-plain-colpass", "u64-plain-colpass"])
+def test_c3_full_shape(mfhe, orc, dig, arith, prefetch):
+    _run_ntt_config(mfhe, orc, dig, "c3", arith, prefetch)
 
 
 def test_c3_60bit_primes_full_shape(mfhe, orc, dig):
@@ -151,10 +144,3 @@ def test_c3_encode_ntt_intt_decode_full_shape(mfhe, orc, dig):
            "C3 wide CRT compose (uniform residues, full path)")
     del res, mag, neg
     torch.cuda.empty_cache()
-
-
-@pytest.mark.parametrize("fused,lag", [(1, 8), (1, 12)])
-def test_c3_full_shape_fused_long_lag(mfhe, orc, dig, fused, lag):
-    """The fused plans at the C3 shape with a long pass-2 lag (more polynomials' intermediates in flight per XCD
-    than its L2 holds)."""
-    _run_ntt_config(mfhe, orc, dig, "c3", 0, fused, None, lag)

@@ -544,6 +544,41 @@ def test_wcrt_mfma_matches_valu_and_oracle(mfhe, orc, n, L):
         np.testing.assert_array_equal(outs[1, 0][0], ref)
 
 
+@pytest.mark.parametrize("kind", ["constant", "random"])
+def test_encode_quantize_near_int64_limit(mfhe, small, kind):
+    """The encode's quantization (llround(v * delta), batched_encoder.cu:125-152) runs fused into the W-CRT digitize
+    (MFHE_OPT_WCRT_MFMA 1, default: an exact FP64 centred reduction of round(v * delta)) or as rns_decompose's
+    int64 llround + the dense GEMM (mode 3).  Both are exact on the reference's llround range |v * delta| < 2^63
+    (mfhe.h mfhe_encode); here with values up to 2^62.9 / delta (a constant message lands as one coefficient of
+    that size per lane) they agree bit for bit."""
+    import torch
+    n, ctx, h = small
+    n2 = n * n
+    rng = np.random.default_rng(11)
+    big = 2.0 ** 62.9 / 2.0 ** 35
+    if kind == "constant":
+        msg = np.full(512 * n2, big * (1 - 1j), np.complex128)
+    else:
+        msg = (rng.uniform(-big, big, 512 * n2) + 1j * rng.uniform(-big, big, 512 * n2)) / 4
+    mt = torch.from_numpy(msg.view(np.float64).copy()).cuda()
+    words = 512 * 11 * n2
+    outs = {}
+    prev = ctx.get_option(mfhe.OPT_WCRT_MFMA)
+    try:
+        for mf in (1, 3, 0):
+            ctx.set_option(mfhe.OPT_WCRT_MFMA, mf)
+            re_ = torch.empty(words, dtype=torch.int64, device="cuda")
+            im_ = torch.empty_like(re_)
+            ctx.encode(mt, re_, im_)
+            torch.cuda.synchronize()
+            outs[mf] = (mfhe.to_host_u64(re_), mfhe.to_host_u64(im_))
+    finally:
+        ctx.set_option(mfhe.OPT_WCRT_MFMA, prev)
+    for mf in (3, 0):
+        np.testing.assert_array_equal(outs[1][0], outs[mf][0])
+        np.testing.assert_array_equal(outs[1][1], outs[mf][1])
+
+
 @pytest.mark.parametrize("n,log_n,L", [(8, 3, 11), (64, 6, 11), (16, 4, 3)])
 def test_layout_transforms_vs_oracle(mfhe, orc, n, log_n, L):
     """matrix_to_poly_kernel / poly_to_matrix_kernel (HE.cu:1330-1368): matrix-major [phi][L][n*n] <->

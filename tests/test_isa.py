@@ -9,6 +9,7 @@ instruction mix and wait immediates; the library also refuses the kernel at run 
 (ntt_plans.hpp col_db_usable).  Needs only the built library and ROCm's llvm tools (no GPU).
 """
 import collections
+import functools
 import re
 import subprocess
 import tempfile
@@ -22,9 +23,12 @@ LLVM = Path("/opt/rocm/lib/llvm/bin")
 MAGIC = b"__CLANG_OFFLOAD_BUNDLE__"
 
 
-def _kernel_asm(symbol_re: str) -> str:
+@functools.lru_cache(maxsize=1)
+def _disassembly() -> tuple:
+    """llvm-objdump of every gfx950 code object in libmfhe.so (one offload bundle per translation unit)."""
     if not LIB.exists() or not (LLVM / "llvm-objdump").exists():
         pytest.skip("libmfhe.so or ROCm llvm tools missing")
+    out = []
     with tempfile.TemporaryDirectory() as td:
         td = Path(td)
         fb = td / "fb.bin"
@@ -39,10 +43,16 @@ def _kernel_asm(symbol_re: str) -> str:
                                 "--targets=hipv4-amdgcn-amd-amdhsa--gfx950", f"--output={co}"], capture_output=True)
             if r.returncode or not co.exists() or co.stat().st_size == 0:
                 continue
-            dis = subprocess.run([str(LLVM / "llvm-objdump"), "-d", str(co)], capture_output=True, text=True).stdout
-            m = re.search(r"^[0-9a-f]+ <(" + symbol_re + r")>:\n(.*?)(?:\n\n|\Z)", dis, re.S | re.M)
-            if m:
-                return m.group(2)
+            out.append(subprocess.run([str(LLVM / "llvm-objdump"), "-d", str(co)], capture_output=True,
+                                      text=True).stdout)
+    return tuple(out)
+
+
+def _kernel_asm(symbol_re: str) -> str:
+    for dis in _disassembly():
+        m = re.search(r"^[0-9a-f]+ <(" + symbol_re + r")>:\n(.*?)(?:\n\n|\Z)", dis, re.S | re.M)
+        if m:
+            return m.group(2)
     pytest.fail(f"kernel {symbol_re} not found in {LIB}")
 
 
@@ -103,3 +113,34 @@ def test_digitize_loads_are_not_serialised(kernel):
                 serial += 1
     assert loads >= 2, (loads, kernel)
     assert serial <= 2, f"{serial} of {loads} loads waited for at once in {kernel}"
+
+
+@pytest.mark.parametrize("D,mode", [(5, 1), (6, 1), (5, 2), (6, 2)])
+def test_wcrt_ring_gemm_counted_waits(D, mode):
+    """mod_gemm_mfma_ring_kernel<D, MODE, false> (gemm.hip), the default factored forward (MODE 1) and inverse
+    (MODE 2) W-CRT GEMM: its K loop waits for stage s with a counted `s_waitcnt vmcnt(D)` / `vmcnt(2D)` that leaves
+    the next stages' D DMA instructions each in flight.  Pinned: D DMAs per 32-k stage (K = 256: 8
+    stages, fully unrolled), no scratch traffic, no store and at most one other vector load between the first DMA
+    and the last barrier of the K loop (an extra op issued there can only make a counted wait stricter), and only
+    the immediates 0, D and 2D there.  The library also refuses a spilling ring kernel at run time (ring_usable)."""
+    asm = _kernel_asm(r"_ZN4mfhe25mod_gemm_mfma_ring_kernelILi%dELi%dELb0E[^>]*" % (D, mode))
+    lines = asm.split("\n")
+    ops = collections.Counter(re.findall(r"^\s+((?:global|buffer|flat|scratch)_[a-z0-9_]+)", asm, re.M))
+    assert not any(k.startswith("scratch_") for k in ops), ops
+    dma = [i for i, ln in enumerate(lines) if "global_load_lds_dwordx4" in ln]
+    assert len(dma) == 8 * D, (len(dma), D)
+    bar = [i for i, ln in enumerate(lines) if "s_barrier" in ln]
+    region = lines[dma[0]:bar[-1] + 1]
+    other = [ln for ln in region if re.search(r"\b(global|buffer|flat)_", ln) and "global_load_lds" not in ln]
+    assert not any("store" in ln or "atomic" in ln for ln in other), other
+    assert len(other) <= 1, other
+    waits = {int(v) for ln in region for v in re.findall(r"vmcnt\((\d+)\)", ln)}
+    assert waits <= {0, D, 2 * D} and {D, 2 * D} <= waits, waits
+    assert len(bar) == 8, len(bar)   # one barrier per stage: the prologue's and seven in the loop
+
+
+def test_wcrt_ring_gemm_no_one_ahead_instantiation_at_d6():
+    """pipe 3 (one-ahead A fragment) runs at D <= 5 only: its D = 6 form spills."""
+    for mode in (0, 1, 2):
+        with pytest.raises(BaseException):
+            _kernel_asm(r"_ZN4mfhe25mod_gemm_mfma_ring_kernelILi6ELi%dELb1E[^>]*" % mode)
