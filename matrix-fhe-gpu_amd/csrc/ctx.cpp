@@ -653,7 +653,7 @@ extern "C" int mfhe_ctx_set_option(mfhe_ctx* c, int opt, int64_t v) {
             c->ntt_chunk_bytes = v;
             return MFHE_OK;
         case MFHE_OPT_NTT_PLAN:
-            if (v < 0 || v > 2) return set_error(MFHE_EINVAL, "plan must be 0, 1 or 2");
+            if (v < 0 || v > 3) return set_error(MFHE_EINVAL, "plan must be 0, 1, 2 or 3");
             c->ntt_plan = (int)v;
             return MFHE_OK;
         case MFHE_OPT_NTT_WG_PER_CU:

@@ -25,6 +25,10 @@ namespace mfhe {
 #define MFHE_NTT_CPOL_INV_COL_OUT MFHE_NTT_CPOL_OUT   // the inverse's last (column) pass output stores
 #endif
 
+#ifndef MFHE_NTT_U64_COLDB_WAVES
+#define MFHE_NTT_U64_COLDB_WAVES 4   // single-buffer (U64) column pass: waves per SIMD the registers must allow (4: 128 VGPRs)
+#endif
+
 #ifndef MFHE_NTT_COLDB_NG
 #define MFHE_NTT_COLDB_NG 16   // columns per tile: 16 (128-B row segments, 2 workgroups/CU) or 32 (256 B, 1/CU)
 #endif
@@ -39,6 +43,7 @@ struct ColDb {
     static constexpr int BUF = NG * GS;                // u64 words per tile buffer (exchange layout, 34,944 B)
     static constexpr size_t LDS_BYTES = 2 * (size_t)BUF * sizeof(uint64_t);
     static constexpr size_t LDS_BYTES_U64 = LDS_BYTES + 512 * sizeof(uint64_t);   // + the U64 twiddle table
+    static constexpr size_t LDS_BYTES_SB_U64 = (size_t)BUF * sizeof(uint64_t) + 512 * sizeof(uint64_t);   // one buffer
     static constexpr int kDmaOps = 256 * NG * 8 / (NT * 16);  // 16-B DMA instructions per thread per tile (8)
     static_assert(Gm::NR == 2 && TG == 16, "two rounds of four stages");
     static_assert(NG == 16 || NG == 32, "16 or 32 columns per tile");
@@ -72,9 +77,10 @@ __device__ __forceinline__ void lds_barrier() { asm volatile("s_waitcnt lgkmcnt(
 // then the raw intermediate (F64: centred doubles; U64: [0, 2q)) stored to base (plain stores, R per thread).
 // tw0: tw[1..15] of the limb (shared), tw1: this thread's round-1 twiddles ((16 + tau) << e) + j.  TW0 / TW1:
 // anything indexable by [0, 15) giving A::Tw -- register arrays (F64), LDS table views (U64).
-template <class A, class TW0, class TW1>
+template <class A, class TW0, class TW1, class HOOK>
 __device__ __forceinline__ void coldb_tile(uint64_t* buf, uint32_t gl, uint32_t tau, const LimbConst& lc,
-                                           const TW0& tw0, const TW1& tw1, uint64_t* base, uint32_t off0, int logS) {
+                                           const TW0& tw0, const TW1& tw1, uint64_t* base, uint32_t off0, int logS,
+                                           HOOK&& after_reads) {
     using C = ColDb;
     using Gm = C::Gm;
     uint64_t* my = buf + (size_t)gl * C::GS;
@@ -97,6 +103,7 @@ __device__ __forceinline__ void coldb_tile(uint64_t* buf, uint32_t gl, uint32_t 
     lds_barrier();
 #pragma unroll
     for (int k = 0; k < C::R; ++k) x[k] = ar.round_reduce(A::from_raw(my[Gm::pad(Gm::g_of(1, tau, k))]));
+    after_reads();   // single-buffer kernel: every thread's reads are done -> the next tile's DMA may land here
     // round 1: stages 4..7, twiddles per thread
     static_for<0, 4>([&](auto bi) {
         constexpr int bb = 3 - decltype(bi)::value, e = 3 - bb, half = 1 << bb;
@@ -136,10 +143,10 @@ struct Tw1U {
 // The inverse table has the forward one's shape, so tw0 / tw1 are coldb_twiddles of itw: round-1 stage bb uses
 // itw[2^(7-bb) + (tau << (3-bb)) + m] = tw1[2^e - 1 + m], round-0 stage bb uses itw[2^(3-bb) + m] = tw0[2^e - 2 + m + 1]
 // with e = 3 - bb.
-template <class A, class TW0, class TW1>
+template <class A, class TW0, class TW1, class HOOK>
 __device__ __forceinline__ void coldb_tile_inv(uint64_t* buf, uint32_t gl, uint32_t tau, const LimbConst& lc,
                                                typename A::Tw ninv, const TW0& tw0, const TW1& tw1, uint64_t* base,
-                                               uint32_t off0, int logS) {
+                                               uint32_t off0, int logS, HOOK&& after_reads) {
     using C = ColDb;
     using Gm = C::Gm;
     uint64_t* my = buf + (size_t)gl * C::GS;
@@ -164,6 +171,7 @@ __device__ __forceinline__ void coldb_tile_inv(uint64_t* buf, uint32_t gl, uint3
     lds_barrier();
 #pragma unroll
     for (int k = 0; k < C::R; ++k) x[k] = A::from_raw(my[Gm::pad(Gm::g_of(0, tau, k))]);
+    after_reads();
     // round 0: stages 3..0 (register bits 0..3); executed stages 4..7 of the pass: 4, 6 lazy, 5 reducing, and the
     // s = 0 stage: X = (u + v) n^-1, Y = (u - v) itw[1] (itw[1] carries n^-1)
     static_for<0, 4>([&](auto bi) {
@@ -219,8 +227,12 @@ __device__ __forceinline__ void coldb_twiddles(const double* tw, uint32_t tau, d
 // A = ArithF64: the limb's twiddles in registers (tw0 by scalar loads); A = ArithU64: the limb's table tw[0, 256)
 // and its Shoup companions DMA'd into LDS (4 KiB after the two tile buffers) -- 30 (w, w') pairs per thread do
 // not fit beside the U64 butterflies' registers, and per-butterfly global loads were the r02 U64 pass's stall.
-template <class A, class TS, bool INV = false>
-__global__ __launch_bounds__(ColDb::NT, 1) void ntt_col_db_kernel(PassArgs<TS> a) {
+// SB (single buffer, the U64 default): one tile buffer; the next tile's DMA is issued once every thread has read the
+// current tile's last LDS image (after the exchange), so it lands during the second round and the stores.  39 KiB of
+// LDS and <= 128 VGPRs (MFHE_NTT_U64_COLDB_WAVES): 4 workgroups per CU instead of 2 -- the U64 pass is VALU-bound (busy
+// 0.70 at 1.5 waves/SIMD, profiles/r03_ntt_sq_pmc.txt) and needs the waves more than the longer DMA lead.
+template <class A, class TS, bool INV = false, bool SB = false>
+__global__ __launch_bounds__(ColDb::NT, SB ? MFHE_NTT_U64_COLDB_WAVES : 1) void ntt_col_db_kernel(PassArgs<TS> a) {
     using C = ColDb;
     constexpr bool U = std::is_same<A, ArithU64>::value;
     extern __shared__ __attribute__((aligned(16))) uint64_t lds[];
@@ -234,7 +246,7 @@ __global__ __launch_bounds__(ColDb::NT, 1) void ntt_col_db_kernel(PassArgs<TS> a
         return tile_loc<C::LOG_G, C::NG, true, true>(a.data, a.batch, a.nl, a.start_limb, a.logN, 0, xcd_remap(l, nb), gl);
     };
     auto tile_ptr = [&](const TileLoc& L) { return (const char*)(L.base + (L.off0 - gl)); };
-    uint64_t* tabw = lds + 2 * C::BUF;   // U64: [0, 256) values, [256, 512) Shoup companions
+    uint64_t* tabw = lds + (SB ? 1 : 2) * C::BUF;   // U64: [0, 256) values, [256, 512) Shoup companions
     typedef __attribute__((address_space(3))) void* lds_vp;
 
     TileLoc L0 = locate(lt);
@@ -281,38 +293,54 @@ __global__ __launch_bounds__(ColDb::NT, 1) void ntt_col_db_kernel(PassArgs<TS> a
                 vm_wait<0>();   // table landed for this wave (published by the barrier below)
             }
         }
-        lds_barrier();   // every thread is done with the other buffer (previous tile's exchange reads)
         uint64_t* nbase = base;
         uint32_t noff0 = off0;
         int nmod = lmod;
+        const char* ntile = nullptr;   // the next tile's first row (DMA source)
         if (more) {
             const TileLoc Ln = locate(nlt);
             nbase = Ln.base;
             noff0 = Ln.off0;
             nmod = Ln.mod;
-            coldb_dma(tile_ptr(Ln), row_bytes, lds + (cur ^ 1) * C::BUF, w, lane);
+            ntile = tile_ptr(Ln);
         }
-        // this thread's part of tile t has landed: newer than its DMA are the previous tile's R stores and the
-        // next tile's DMA instructions
-        if (first) {
-            if (more) vm_wait<C::kDmaOps>();
-            else vm_wait<0>();
+        if constexpr (!SB) {
+            lds_barrier();   // every thread is done with the other buffer (previous tile's exchange reads)
+            if (more) coldb_dma(ntile, row_bytes, lds + (cur ^ 1) * C::BUF, w, lane);
+            // this thread's part of tile t has landed: newer than its DMA are the previous tile's R stores and the
+            // next tile's DMA instructions
+            if (first) {
+                if (more) vm_wait<C::kDmaOps>();
+                else vm_wait<0>();
+            } else {
+                if (more) vm_wait<C::R + C::kDmaOps>();
+                else vm_wait<C::R>();
+            }
         } else {
-            if (more) vm_wait<C::R + C::kDmaOps>();
+            // single buffer: tile t's DMA was issued during tile t - 1, before that tile's R stores
+            if (first) vm_wait<0>();
             else vm_wait<C::R>();
         }
         lds_barrier();   // ... and every other thread's part
         first = false;
 
-        uint64_t* buf = lds + (size_t)cur * C::BUF;
+        uint64_t* buf = lds + (size_t)(SB ? 0 : cur) * C::BUF;
+        auto hook = [&]() {
+            if constexpr (SB) {
+                if (more) {
+                    lds_barrier();   // every thread has read the buffer's last image of tile t
+                    coldb_dma(ntile, row_bytes, lds, w, lane);
+                }
+            }
+        };
         if constexpr (U) {
             const Tw0U t0{tabw, tabw + 256};
             const Tw1U t1{tabw, tabw + 256, tau};
-            if constexpr (INV) coldb_tile_inv<A>(buf, gl, tau, lc, ninv, t0, t1, base, off0, logS);
-            else coldb_tile<A>(buf, gl, tau, lc, t0, t1, base, off0, logS);
+            if constexpr (INV) coldb_tile_inv<A>(buf, gl, tau, lc, ninv, t0, t1, base, off0, logS, hook);
+            else coldb_tile<A>(buf, gl, tau, lc, t0, t1, base, off0, logS, hook);
         } else {
-            if constexpr (INV) coldb_tile_inv<A>(buf, gl, tau, lc, ninv, tw0, tw1, base, off0, logS);
-            else coldb_tile<A>(buf, gl, tau, lc, tw0, tw1, base, off0, logS);
+            if constexpr (INV) coldb_tile_inv<A>(buf, gl, tau, lc, ninv, tw0, tw1, base, off0, logS, hook);
+            else coldb_tile<A>(buf, gl, tau, lc, tw0, tw1, base, off0, logS, hook);
         }
         if (!more) break;
         lt = nlt;

@@ -13,6 +13,7 @@
 
 #include "mfhe_ctx.hpp"
 #include "ntt_coldb.hpp"
+#include "ntt_single14.hpp"
 
 // Groups (contiguous rows) per block-pass workgroup.  N = 2^16: 4 rows (64 threads, 8.7 KiB LDS) rather than 16
 // (256 threads, 34.9 KiB): the block pass gains from residency and 16-row tiles are LDS-bound at 4 per CU;
@@ -37,6 +38,9 @@
 #endif
 #ifndef MFHE_NTT_INV17_SPLIT
 #define MFHE_NTT_INV17_SPLIT 0      // N = 2^17 inverse: 0 = 8 block + 9 column stages; 1 = 9 block + 8 column (DMA pass)
+#endif
+#ifndef MFHE_NTT_U64_COLDB_SB
+#define MFHE_NTT_U64_COLDB_SB 1     // U64 column pass: 1 = single tile buffer, 3 workgroups per CU; 0 = double buffer, 2
 #endif
 #ifndef MFHE_NTT_INV16_PLAIN_NG
 #define MFHE_NTT_INV16_PLAIN_NG 0   // N = 2^16 inverse last pass: 0 = DMA column pass; 16 / 32 = plain column pass (A/B)
@@ -117,23 +121,27 @@ static int launch_pass(const NttJob<TS>& j, int s0, hipStream_t st) {
 // whose kernel spills (scratch loads/stores are vector-memory ops too) would make them too loose.  Checked once
 // per process from the code object's metadata; such a build runs the plain column pass instead
 // (tests/test_isa.py checks the instruction counts of the shipped library).
-template <class A, class TS, bool INV>
+template <class A, class TS, bool INV, bool SB>
 static bool col_db_usable() {
     static int ok = -1;
     if (ok < 0) {
         hipFuncAttributes fa{};
-        ok = hipFuncGetAttributes(&fa, reinterpret_cast<const void*>(ntt_col_db_kernel<A, TS, INV>)) == hipSuccess &&
+        ok = hipFuncGetAttributes(&fa, reinterpret_cast<const void*>(ntt_col_db_kernel<A, TS, INV, SB>)) == hipSuccess &&
              fa.localSizeBytes == 0;
     }
     return ok == 1;
 }
+// U64 runs the single-buffer column pass (3 workgroups per CU; ntt_coldb.hpp SB), FP64 the double buffer
+template <class A>
+constexpr bool col_db_single() { return std::is_same<A, ArithU64>::value && MFHE_NTT_U64_COLDB_SB; }
 
 // column pass with the next tile's DMA in flight (ntt_coldb.hpp), MFHE_OPT_NTT_PREFETCH = 2: the forward's first
 // pass, or (INV) the inverse's last pass
 template <class A, class TS, bool INV>
 static int launch_col_db(const NttJob<TS>& j, hipStream_t st) {
     using C = ColDb;
-    constexpr size_t lds = std::is_same<A, ArithU64>::value ? C::LDS_BYTES_U64 : C::LDS_BYTES;
+    constexpr bool SB = col_db_single<A>();
+    constexpr size_t lds = SB ? C::LDS_BYTES_SB_U64 : std::is_same<A, ArithU64>::value ? C::LDS_BYTES_U64 : C::LDS_BYTES;
     const uint64_t npl = j.batch * (uint64_t)j.nl;
     const uint64_t nb = npl << (j.logN - C::LOG_G - C::LOG_NG);   // NG-column tiles: 2^(logN - 8) / NG per polynomial
     if (nb == 0) return MFHE_OK;
@@ -153,7 +161,7 @@ static int launch_col_db(const NttJob<TS>& j, hipStream_t st) {
     static int occ = 0;
     if (occ == 0) {
         int o = 0;
-        if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&o, ntt_col_db_kernel<A, TS, INV>, C::NT, lds) != hipSuccess ||
+        if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&o, ntt_col_db_kernel<A, TS, INV, SB>, C::NT, lds) != hipSuccess ||
             o < 1)
             o = 1;
         occ = o;
@@ -161,8 +169,39 @@ static int launch_col_db(const NttJob<TS>& j, hipStream_t st) {
     const int per_cu = j.wg_per_cu > 0 ? std::min(j.wg_per_cu, occ) : occ;
     const uint64_t cap = std::max<uint64_t>(8, ((uint64_t)per_cu * j.num_cus) & ~7ull);
     const uint32_t grid = (uint32_t)std::min<uint64_t>(nb, cap);
-    hipLaunchKernelGGL((ntt_col_db_kernel<A, TS, INV>), dim3(grid), dim3(C::NT), lds, st, a);
+    hipLaunchKernelGGL((ntt_col_db_kernel<A, TS, INV, SB>), dim3(grid), dim3(C::NT), lds, st, a);
     MFHE_CHECK_LAUNCH("ntt_col_db_kernel launch");
+    return MFHE_OK;
+}
+
+// N = 2^14, FP64: one pass, one polynomial per workgroup at a time with the next one's loads in flight
+// (ntt_single14.hpp).  Persistent grid of one workgroup per CU (144 KiB of LDS).
+template <bool INV>
+static int launch_s14(const NttJob<TwSrcF>& j, hipStream_t st) {
+    const uint64_t npl = j.batch * (uint64_t)j.nl;
+    if (npl == 0) return MFHE_OK;
+    if (npl >= 0xFFFFFFFFull) return set_error(MFHE_EINVAL, "NTT batch too large for one launch (batch * nlimbs must be < 2^32)");
+    PassArgs<TwSrcF> a{};
+    a.data = j.data;
+    a.tw = j.tw;
+    a.ninv = j.ninv;
+    a.limbs = j.limbs;
+    a.batch = j.batch;
+    a.nl = j.nl;
+    a.start_limb = j.start_limb;
+    a.logN = 14;
+    a.nblocks = (uint32_t)npl;
+    static int occ = 0;
+    if (occ == 0) {
+        int o = 0;
+        if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&o, ntt14_kernel<INV>, S14::NT, S14::LDS_BYTES) != hipSuccess ||
+            o < 1)
+            o = 1;
+        occ = o;
+    }
+    const uint32_t grid = (uint32_t)std::min<uint64_t>(npl, (uint64_t)occ * j.num_cus);
+    hipLaunchKernelGGL((ntt14_kernel<INV>), dim3(grid), dim3(S14::NT), S14::LDS_BYTES, st, a);
+    MFHE_CHECK_LAUNCH("ntt14_kernel launch");
     return MFHE_OK;
 }
 
@@ -218,7 +257,7 @@ static int two_pass_chunk(const NttJob<TS>& c, int pass, hipStream_t st) {
     }
     if constexpr (LOG_GA == 8 && NGA == 16) {
         // the column pass with the next tile's DMA in flight: the forward's first pass, the inverse's second
-        if (pass == (INV ? 1 : 0) && c.prefetch >= 2 && c.limbs && col_db_usable<A, TS, INV>())
+        if (pass == (INV ? 1 : 0) && c.prefetch >= 2 && c.limbs && col_db_usable<A, TS, INV, col_db_single<A>()>())
             return launch_col_db<A, TS, INV>(c, st);
     }
     if (!INV) {
@@ -262,6 +301,10 @@ static int run_phantom(const NttJob<TS>& j, hipStream_t st) {
     // auto: N = 2^14 runs two passes (7 + 7, 8-row block tiles): at C2 +1% forward, +7% inverse over the single
     // pass, which holds one 2^14 polynomial per CU (139 KiB of LDS) and cannot overlap loads with butterflies
     // (profiles/r02_c2_plans2.txt)
+    if constexpr (std::is_same<A, ArithF64>::value) {
+        // N = 2^14: the pipelined single pass (plan 0 = auto, or 3); plan 1 / 2 keep the earlier plans for A/B
+        if (j.logN == 14 && j.limbs && (j.plan == 0 || j.plan == 3)) return launch_s14<INV>(j, st);
+    }
     const bool two = j.logN > 14 || (j.plan == 2 && j.logN >= 12) || (j.plan == 0 && j.logN == 14);
     if (!two) return run_single<A, TS, INV, false>(j, st);
     switch (j.logN) {

@@ -1,0 +1,271 @@
+// ntt_single14.hpp -- N = 2^14 (BASELINE C2) in one pass at 16N bytes per transform, with the next polynomial's
+// loads in flight while the current one computes.  FP64 arithmetic (every q < 2^50).
+//
+// Why.  A 2^14 polynomial is 128 KiB: it fits one CU's LDS, so the whole transform can run in one pass (8N read +
+// 8N write) instead of the two-pass plan's 32N.  The earlier single pass (NttPass, plan 1) measured no faster than
+// two passes because each CU serialised load -> compute -> store: one 1024-thread workgroup per CU (139 KiB LDS),
+// and `__syncthreads()` at every LDS exchange carries a vmcnt(0) that would wait for any prefetch, as do the
+// per-butterfly twiddle loads from global memory (vmcnt is in order).
+//
+// Here nothing in a polynomial's compute touches vector memory, so the next polynomial's 16 loads per thread stay
+// in flight through the whole transform and the current one's 16 stores drain behind the next compute:
+//   * twiddles come from LDS: tw[0, 2048) of the limb (16 KiB, the direct table for stages 0..10) plus
+//     tw[2048 i], i = 1..7; a stage-11..13 twiddle is the product tw[k] = tw[k & 2047] * tw[k & ~2047]
+//     (tw[k] = psi^brev14(k) and brev is additive over disjoint bits), one exact FP64 modmul;
+//   * barriers are `s_waitcnt lgkmcnt(0); s_barrier` (lds_barrier), never __syncthreads();
+//   * the loads go into raw[16] right after raw was converted into x[16]: 32 + 32 VGPRs of data.
+// LDS: 128 KiB of data (no padding: an XOR swizzle makes every exchange access conflict-free) + 16 KiB of table =
+// 144 KiB, so one workgroup of 1024 threads (16 waves) per CU.
+//
+// Layouts (element index j = b13..b0; thread t: lane = t & 63, wave = t >> 6; register k = 4 bits):
+//   L0: k -> b13..b10, t -> b9..b0                                 (global loads / stores: 512 B per wave access)
+//   L1: k -> b9..b6, lane -> b5..b0, wave -> b13..b10
+//   L2: k -> b5..b2, lane -> b1 b0 (lane bits 0, 1), b9..b6 (lane bits 2..5), wave -> b13..b10
+//   L3: k -> b3..b0, lane bits 0..3 -> b8..b5, lane bit 4 -> b4, lane bit 5 -> b9, wave -> b13..b10
+// Forward (CT, stage s pairs bit 13 - s): L0 stages 0-3 | L1 4-7 | L2 8-10 (b2 rides along) | L3 11-13 | -> L0.
+// Inverse (GS): L0 -> L3 stages 13-11 | L2 10-8 | L1 7-4 | L0 3-0 (n^-1 at s = 0).
+// Arithmetic and reduction schedule as in NttPass (ntt_arith.hpp): forward, one centred reduction at the start of
+// every round after the first (rounds of <= 4 stages: |x| < 3q); inverse, lazy GS on every other stage.
+// Reference: phantom fnwt_1d / inwt_1d per polynomial (ntt_core.cu:443-460); same outputs, bit for bit.
+#pragma once
+#include "ntt_coldb.hpp"
+
+#ifndef MFHE_S14_EXP
+#define MFHE_S14_EXP 0   // timing probes (wrong results), never in the product build
+#endif
+
+namespace mfhe {
+
+struct S14 {
+    static constexpr int LOGN = 14, N = 1 << 14, NT = 1024, R = 16;
+    static constexpr int TAB = 2048;   // direct twiddles per limb in LDS (stages 0..10)
+    static constexpr size_t LDS_BYTES = (size_t)N * 8 + (size_t)(TAB + 8) * 8;
+};
+
+// LDS slot of element j.  h XORs b5, b6, b7, b8 into bits 0, 2, 3, {1, 4}: every exchange access (ds_write_b64:
+// 16-lane groups must hit distinct slots mod 16; ds_read_b64: 32-lane groups, distinct mod 32) is conflict-free
+// in all four layouts (checked by tests/test_ntt14_layout.py).
+__device__ __host__ __forceinline__ uint32_t s14_swz(uint32_t j) {
+    const uint32_t h = ((j >> 5) & 1u) | (((j >> 6) & 1u) << 2) | (((j >> 7) & 1u) << 3) | (((j >> 8) & 1u) * 18u);
+    return j ^ h;
+}
+
+template <int LAY>
+__device__ __host__ __forceinline__ uint32_t s14_j(uint32_t t, uint32_t k) {
+    const uint32_t lane = t & 63u, wave = t >> 6;
+    if constexpr (LAY == 0) return (k << 10) | t;
+    else if constexpr (LAY == 1) return (wave << 10) | (k << 6) | lane;
+    else if constexpr (LAY == 2) return (wave << 10) | ((lane >> 2) << 6) | (k << 2) | (lane & 3u);
+    else return (wave << 10) | ((lane >> 5) << 9) | ((lane & 15u) << 5) | (((lane >> 4) & 1u) << 4) | k;
+}
+// j bit held by register bit 0 of each layout
+template <int LAY>
+constexpr int s14_kbase() { return LAY == 0 ? 10 : LAY == 1 ? 6 : LAY == 2 ? 2 : 0; }
+
+// A thread index the compiler cannot see through: every address derived from it is computed where it is used.
+// Without this, LICM hoists the ~130 loop-invariant LDS addresses of the four exchanges and the twiddle reads out
+// of the polynomial loop and keeps them live (VGPRs 128 + 102 spilled).
+__device__ __forceinline__ uint32_t s14_opaque(uint32_t t) {
+    asm volatile("" : "+v"(t));
+    return t;
+}
+
+template <int FROM, int TO>
+__device__ __forceinline__ void s14_exchange(double (&x)[16], double* lds, uint32_t t_) {
+    const uint32_t t = s14_opaque(t_);
+    lds_barrier();   // the previous readers of the buffer are done
+#pragma unroll
+    for (int k = 0; k < 16; ++k) lds[s14_swz(s14_j<FROM>(t, (uint32_t)k))] = x[k];
+    lds_barrier();
+#pragma unroll
+    for (int k = 0; k < 16; ++k) x[k] = lds[s14_swz(s14_j<TO>(t, (uint32_t)k))];
+}
+
+// Twiddle of stage s for the butterfly group whose lower element is j (index 2^s + (j >> (14 - s))), from the LDS
+// tables: direct below 2048, else the product of tab[idx & 2047] and btab[idx >> 11] = tw[idx & ~2047].
+__device__ __forceinline__ double s14_tw(const ArithF64& ar, const double* tab, const double* btab, int s, uint32_t j) {
+    const uint32_t idx = (1u << s) + (j >> (14 - s));
+    if (s <= 10) return tab[idx];
+    return ar.mulmod(tab[idx & 2047u], btab[idx >> 11]);
+}
+
+// CT stages on register bits BB_HI .. BB_LO (descending) of layout LAY
+template <int LAY, int BB_HI, int BB_LO>
+__device__ __forceinline__ void s14_ct_round(double (&x)[16], const ArithF64& ar, const double* tab,
+                                             const double* btab, uint32_t t_) {
+    const uint32_t t = s14_opaque(t_);
+    static_for<0, BB_HI - BB_LO + 1>([&](auto ic) {
+        constexpr int bb = BB_HI - decltype(ic)::value;
+        constexpr int b = s14_kbase<LAY>() + bb, s = 13 - b, half = 1 << bb;
+        // one twiddle per group of butterflies sharing the register bits above bb
+        double w[16 >> (bb + 1)];
+#pragma unroll
+        for (int g = 0; g < (16 >> (bb + 1)); ++g) w[g] = s14_tw(ar, tab, btab, s, s14_j<LAY>(t, (uint32_t)(g << (bb + 1))));
+#pragma unroll
+        for (int k = 0; k < 16; ++k) {
+            if (k & half) continue;
+            ar.ct(x[k], x[k + half], w[k >> (bb + 1)]);
+        }
+    });
+}
+
+// GS stages on register bits BB_LO .. BB_HI (ascending) of layout LAY; lazy on odd s, reducing on even s, and the
+// s = 0 stage: X = (u + v) n^-1, Y = (u - v) itw[1] (itw[1] carries n^-1)
+template <int LAY, int BB_LO, int BB_HI>
+__device__ __forceinline__ void s14_gs_round(double (&x)[16], const ArithF64& ar, const double* tab,
+                                             const double* btab, double w1, double ninv, uint32_t t_) {
+    const uint32_t t = s14_opaque(t_);
+    static_for<0, BB_HI - BB_LO + 1>([&](auto ic) {
+        constexpr int bb = BB_LO + decltype(ic)::value;
+        constexpr int b = s14_kbase<LAY>() + bb, s = 13 - b, half = 1 << bb;
+        if constexpr (s == 0) {
+#pragma unroll
+            for (int k = 0; k < 16; ++k) {
+                if (k & half) continue;
+                double u = x[k], v = x[k + half];
+                ar.gs_lazy(u, v, w1);
+                x[k] = ar.mulmod(u, ninv);
+                x[k + half] = v;
+            }
+        } else {
+            double w[16 >> (bb + 1)];
+#pragma unroll
+            for (int g = 0; g < (16 >> (bb + 1)); ++g)
+                w[g] = s14_tw(ar, tab, btab, s, s14_j<LAY>(t, (uint32_t)(g << (bb + 1))));
+#pragma unroll
+            for (int k = 0; k < 16; ++k) {
+                if (k & half) continue;
+                if constexpr (s % 2 == 1) ar.gs_lazy(x[k], x[k + half], w[k >> (bb + 1)]);
+                else ar.gs(x[k], x[k + half], w[k >> (bb + 1)]);
+            }
+        }
+    });
+}
+
+template <bool INV>
+__global__ __launch_bounds__(S14::NT, 1) void ntt14_kernel(PassArgs<TwSrcF> a) {
+    extern __shared__ __attribute__((aligned(16))) uint64_t lds_raw[];
+    double* lds = (double*)lds_raw;
+    double* tab = lds + S14::N;          // [2048]: tw[0, 2048) of the limb (inverse: itw, entry 1 without n^-1)
+    double* btab = tab + S14::TAB;       // [8]: tw[2048 i]
+    const uint32_t t = threadIdx.x;
+    const uint32_t nb = a.nblocks;       // polynomials (batch * nl)
+    uint32_t lt = blockIdx.x;
+    if (lt >= nb) return;
+    const uint32_t bt = (uint32_t)a.batch;
+    auto poly = [&](uint32_t l, int* mod) {
+        const uint32_t v = xcd_remap(l, nb);   // limb-major: v = limb * batch + b
+        const uint32_t li = v / bt, b = v - li * bt;
+        *mod = a.start_limb + (int)li;
+        const uint64_t* p = a.data + (((uint64_t)b * (uint64_t)a.nl + li) << S14::LOGN);
+        // workgroup-uniform: say so, so the accesses are SGPR base + lane offset
+        const uint64_t pu = (uint64_t)p;
+        return (uint64_t*)(((uint64_t)(uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)(pu >> 32)) << 32) |
+                           (uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)pu));
+    };
+    auto load = [&](const uint64_t* base, uint64_t (&raw)[16]) {
+        const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc((void*)base, 0, 0x7FFFFFFF, 0x00020000);
+#pragma unroll
+        for (int k = 0; k < 16; ++k)
+            raw[k] = __builtin_bit_cast(uint64_t, __builtin_amdgcn_raw_buffer_load_b64(rs, (int)(((k << 10) | t) * 8u), 0, 0));
+    };
+    int mod = 0, tmod = -1;
+    uint64_t* base = poly(lt, &mod);
+    uint64_t raw[16];
+    load(base, raw);
+    ArithF64 ar(LimbConst{});
+    double w1 = 0.0, ninv = 0.0;
+    while (true) {
+        const uint32_t nlt = lt + gridDim.x;
+        const bool more = nlt < nb;   // workgroup-uniform
+        if (mod != tmod) {
+            // the limb's constants by scalar loads; its twiddle table into LDS (a vector load + wait, once per limb)
+            tmod = mod;
+            const __attribute__((address_space(4))) LimbConst* cl =
+                (const __attribute__((address_space(4))) LimbConst*)a.limbs + mod;
+            LimbConst lc;
+            lc.q = cl->q;
+            lc.qf = cl->qf;
+            lc.qinv = cl->qinv;
+            ar = ArithF64(lc);
+            typedef const __attribute__((address_space(4))) double* cd_t;
+            const double* tw = a.tw.p + ((size_t)mod << S14::LOGN);
+            if constexpr (INV) {
+                w1 = ((cd_t)tw)[1];
+                ninv = ((cd_t)a.ninv.p)[mod];
+            }
+            lds_barrier();   // every thread is done with the previous limb's table
+            const double2 v = ((const double2*)tw)[t];   // tw[2t], tw[2t + 1]
+            ((double2*)tab)[t] = v;
+            if (t < 8) btab[t] = t ? tw[t << 11] : 1.0;
+            if constexpr (INV) {
+                // itw[1] carries n^-1 (ctx.cpp build_ct_tables): the table needs the plain power psi^-brev(1)
+                if (t == 0) tab[1] = ar.reduce(ar.mulmod(v.y, (double)S14::N));
+            }
+            lds_barrier();
+        }
+        double x[16];
+#pragma unroll
+        for (int k = 0; k < 16; ++k) x[k] = ArithF64::from_u64(raw[k]);
+        uint64_t* nbase = base;
+        int nmod = mod;
+        if (more) {
+            nbase = poly(nlt, &nmod);
+#if MFHE_S14_EXP != 1
+            load(nbase, raw);   // in flight through the whole transform below
+#endif
+        }
+#if MFHE_S14_EXP >= 2   // timing probes only (wrong results): 2 = no butterflies, 3 = no butterflies, no exchanges
+        if (true) {
+#if MFHE_S14_EXP == 2
+            s14_exchange<0, 1>(x, lds, t);
+            s14_exchange<1, 2>(x, lds, t);
+            s14_exchange<2, 3>(x, lds, t);
+            s14_exchange<3, 0>(x, lds, t);
+#endif
+        } else
+#endif
+        if constexpr (!INV) {
+            s14_ct_round<0, 3, 0>(x, ar, tab, btab, t);
+            s14_exchange<0, 1>(x, lds, t);
+#pragma unroll
+            for (int k = 0; k < 16; ++k) x[k] = ar.round_reduce(x[k]);
+            s14_ct_round<1, 3, 0>(x, ar, tab, btab, t);
+            s14_exchange<1, 2>(x, lds, t);
+#pragma unroll
+            for (int k = 0; k < 16; ++k) x[k] = ar.round_reduce(x[k]);
+            s14_ct_round<2, 3, 1>(x, ar, tab, btab, t);
+            s14_exchange<2, 3>(x, lds, t);
+#pragma unroll
+            for (int k = 0; k < 16; ++k) x[k] = ar.round_reduce(x[k]);
+            s14_ct_round<3, 2, 0>(x, ar, tab, btab, t);
+            s14_exchange<3, 0>(x, lds, t);
+        } else {
+            s14_exchange<0, 3>(x, lds, t);
+            s14_gs_round<3, 0, 2>(x, ar, tab, btab, w1, ninv, t);
+            s14_exchange<3, 2>(x, lds, t);
+            s14_gs_round<2, 1, 3>(x, ar, tab, btab, w1, ninv, t);
+            s14_exchange<2, 1>(x, lds, t);
+            s14_gs_round<1, 0, 3>(x, ar, tab, btab, w1, ninv, t);
+            s14_exchange<1, 0>(x, lds, t);
+            s14_gs_round<0, 0, 3>(x, ar, tab, btab, w1, ninv, t);
+        }
+#if MFHE_S14_EXP == 1   // timing probe only: compute without memory traffic (loads once, never stores)
+        if (lt == 0xFFFFFFFFu)
+#endif
+        {
+            const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(base, 0, 0x7FFFFFFF, 0x00020000);
+#pragma unroll
+            for (int k = 0; k < 16; ++k)
+                __builtin_amdgcn_raw_buffer_store_b64(
+                    __builtin_bit_cast(__attribute__((ext_vector_type(2))) unsigned, ar.canon(x[k])), rs,
+                    (int)(((k << 10) | t) * 8u), 0, MFHE_NTT_CPOL_OUT);
+        }
+        if (!more) break;
+        lt = nlt;
+        base = nbase;
+        mod = nmod;
+    }
+}
+
+}  // namespace mfhe

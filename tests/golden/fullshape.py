@@ -1,4 +1,4 @@
-"""Full-shape parity configurations (BASELINE.json configs C2, C3, C5-shard) and their digests.
+"""Full-shape parity configurations (BASELINE.json configs C2, C3, C4-shard, C5-shard) and their digests.
 
 Test infrastructure.  The BASELINE shapes are too large to commit as vectors (C3 is 4 GiB per buffer,
 the C5 shard 16 GiB), so the CPU oracle's outputs are committed as SHA-256 digests instead
@@ -33,6 +33,8 @@ NTT_CONFIGS = {
     "c3": dict(log_n=16, L=8, bits=50, batch=1024, start=0, nl=8, seed=SEED0 + 3, kinds=("fwd", "inv")),
     # the same shape with 60-bit primes: the U64 (Harvey/Shoup) arithmetic path
     "c3u60": dict(log_n=16, L=8, bits=60, batch=1024, start=0, nl=8, seed=SEED0 + 0x33, kinds=("fwd", "inv")),
+    # configs[3] residue shard: N = 2^16, 16 moduli, batch 1024; GPU 1 of 4 owns limbs 4..7
+    "c4shard": dict(log_n=16, L=16, bits=50, batch=1024, start=4, nl=4, seed=SEED0 + 4, kinds=("fwd", "inv")),
     # configs[4] residue shard: N = 2^17, 32 moduli, batch 4096; GPU 1 of 8 owns limbs 4..7
     "c5shard": dict(log_n=17, L=32, bits=50, batch=4096, start=4, nl=4, seed=SEED0 + 5, kinds=("fwd",)),
 }

@@ -63,19 +63,28 @@ def c3_pipeline() -> dict:
 
 
 def main():
-    res = {}
-    meta = {}
+    """No arguments: every configuration.  With names (e.g. `c4shard`): only those, merged into the committed
+    digests.npz / digests.json (the other entries are kept as they are)."""
+    only = set(sys.argv[1:])
+    res, meta = {}, {}
+    if only:
+        with np.load(HERE / "digests.npz") as z:
+            res = {k: z[k] for k in z.files}
+        meta = json.loads((HERE / "digests.json").read_text())
     for name, cfg in F.NTT_CONFIGS.items():
+        if only and name not in only:
+            continue
         t = time.time()
         d = ntt_digests(name, cfg)
         res.update(d)
         meta[name] = {k: F.top_digest(v) for k, v in d.items()}
         print(f"{name}: {time.time() - t:.1f} s", meta[name], flush=True)
-    t = time.time()
-    d = c3_pipeline()
-    res.update(d)
-    meta["c3pipe"] = {k: F.top_digest(v) for k, v in d.items() if k != "c3pipe_W"}
-    print(f"c3pipe: {time.time() - t:.1f} s", meta["c3pipe"], flush=True)
+    if not only or "c3pipe" in only:
+        t = time.time()
+        d = c3_pipeline()
+        res.update(d)
+        meta["c3pipe"] = {k: F.top_digest(v) for k, v in d.items() if k != "c3pipe_W"}
+        print(f"c3pipe: {time.time() - t:.1f} s", meta["c3pipe"], flush=True)
     np.savez_compressed(HERE / "digests.npz", **res)
     (HERE / "digests.json").write_text(json.dumps(meta, indent=1) + "\n")
 

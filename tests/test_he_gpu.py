@@ -263,13 +263,31 @@ def test_keygen_bit_exact_reference_geometry(mfhe, orc):
 
 
 def test_encrypt_decrypt_vs_oracle(mfhe, orc, small):
-    import torch
     n, ctx, h = small
-    words = 512 * 11 * n * n
+    _encrypt_decrypt_vs_oracle(mfhe, orc, n, ctx, h, RNS)
+
+
+def test_encrypt_decrypt_vs_oracle_c4_moduli(mfhe, orc):
+    """The same bit-exact check with BASELINE C4's parameter set (test_encode_encrypt_decrypt_decode_wcrt.cu:29-110):
+    L = 16 primes of 35 bits, q = 1 mod 2^8 * 771, at small n (VERDICT r03 #7)."""
+    from bench import gen_moduli
+    moduli = gen_moduli(35, 197376, 16)
+    n = 8
+    ctx = mfhe.Context(moduli, 3, CONV)
+    h = orc.HE(n, moduli, 2.0 ** 35)
+    _encrypt_decrypt_vs_oracle(mfhe, orc, n, ctx, h, moduli)
+    ctx.close()
+
+
+def _encrypt_decrypt_vs_oracle(mfhe, orc, n, ctx, h, moduli):
+    import torch
+    Lq = len(moduli)
+    words = 512 * Lq * n * n
     rng = np.random.default_rng(3)
-    m_re, m_im = _rand_mat(rng, n), _rand_mat(rng, n)
+    qm = np.array(moduli, np.uint64)[None, :, None]
+    m_re, m_im = ((rng.integers(0, 2 ** 63, (512, Lq, n * n), dtype=np.uint64) % qm).ravel() for _ in range(2))
     sk_ref = h.keygen()
-    sk = torch.empty(512 * 11 * n, dtype=torch.int64, device="cuda")
+    sk = torch.empty(512 * Lq * n, dtype=torch.int64, device="cuda")
     ctx.keygen(sk)
     torch.cuda.synchronize()
     np.testing.assert_array_equal(mfhe.to_host_u64(sk), sk_ref)
@@ -289,15 +307,15 @@ def test_encrypt_decrypt_vs_oracle(mfhe, orc, small):
     # e), so the oracle's inverse W-CRT of (b_dev - b_orc) must be a noise difference in {-1, 0, +1}, the same
     # integer in every limb, nonzero only where the unrounded Box-Muller sample sits on a .5 rounding boundary
     # (HE.cu:605-627: the only step where device libm and glibc may differ)
-    n2, Lq = n * n, len(RNS)
-    q_el = np.array(RNS, dtype=object)[(np.arange(words) // n2) % Lq]
-    q3 = np.array(RNS, np.uint64)[None, :, None]
+    n2 = n * n
+    q_el = np.array(moduli, dtype=object)[(np.arange(words) // n2) % Lq]
+    q3 = np.array(moduli, np.uint64)[None, :, None]
     noise = []
     for got, want in ((gre, ore), (gim, oim)):
         d = ((got[:words].astype(object) - want[:words].astype(object)) % q_el).astype(np.uint64)
         poly, de = np.zeros_like(d), np.zeros_like(d)
         orc.L.orc_matrix_to_poly(P(d), P(poly), n, Lq, 512)
-        orc.L.orc_wntt_inverse_matrix(P(poly), P(de), n, Lq, 512, P(U64(RNS)), orc.L.orc_he_VinvT(h.h))
+        orc.L.orc_wntt_inverse_matrix(P(poly), P(de), n, Lq, 512, P(U64(moduli)), orc.L.orc_he_VinvT(h.h))
         de = de.reshape(512, Lq, n2)
         sgn = np.where(de == 0, 0, np.where(de == 1, 1, np.where(de == q3 - 1, -1, 99)))
         assert (sgn != 99).all(), "ciphertexts differ by more than a +-1 noise step"

@@ -283,6 +283,46 @@ def test_two_pass_plans_and_chunking(mfhe, orc, log_n):
         np.testing.assert_array_equal(mfhe.to_host_u64(d), data)
 
 
+@pytest.mark.parametrize("batch,nl,start", [(1, 1, 0), (5, 3, 1), (300, 2, 2), (1023, 1, 3), (64, 4, 0)])
+def test_single_pass_14_matches_oracle_and_other_plans(mfhe, orc, batch, nl, start):
+    """N = 2^14 pipelined single pass (ntt_single14.hpp, plan 0 = auto / 3; FP64): bit-exact against the oracle
+    (forward and the inverse of random data), exact round trip, and equal to the two-pass (2) and the plain single
+    pass (1).  Batches that leave some workgroups with one polynomial, several, or a limb change inside their
+    polynomial walk (the LDS twiddle table is reloaded), a limb sub-range, and the largest primes < 2^50 with the
+    all-(q - 1) input as the first polynomial."""
+    import torch
+    log_n, N = 14, 1 << 14
+    moduli = orc.gen_primes(50, 4 * N, start + nl)
+    ctx = mfhe.Context(moduli, log_n)
+    assert ctx.info().arith == mfhe.ARITH_F64
+    sub = moduli[start:start + nl]
+    rng = np.random.default_rng(batch * 7 + nl)
+    data = rand_residues(rng, batch, sub, N)
+    data[:nl * N] = (np.array(sub, np.uint64)[:, None] - np.uint64(1)).repeat(N, axis=1).ravel()
+    want_f = orc.phantom_fwd(data, nl, log_n, sub) if batch <= 300 else None
+    got = {}
+    for plan in (0, 3, 2, 1):
+        ctx.set_option(mfhe.OPT_NTT_PLAN, plan)
+        d = mfhe.to_device_u64(data)
+        ctx.ntt_fwd(d, batch=batch, start_limb=start, nlimbs=nl)
+        torch.cuda.synchronize()
+        got[plan] = mfhe.to_host_u64(d)
+        ctx.ntt_inv(d, batch=batch, start_limb=start, nlimbs=nl)
+        torch.cuda.synchronize()
+        np.testing.assert_array_equal(mfhe.to_host_u64(d), data)
+    if want_f is not None:
+        np.testing.assert_array_equal(got[0], want_f)
+    for plan in (3, 2, 1):
+        np.testing.assert_array_equal(got[plan], got[0])
+    # the inverse of arbitrary residues (not the forward's output) against the oracle
+    if batch <= 64:
+        ctx.set_option(mfhe.OPT_NTT_PLAN, 0)
+        d = mfhe.to_device_u64(data)
+        ctx.ntt_inv(d, batch=batch, start_limb=start, nlimbs=nl)
+        torch.cuda.synchronize()
+        np.testing.assert_array_equal(mfhe.to_host_u64(d), orc.phantom_inv(data, nl, log_n, sub))
+
+
 def test_fused_option_removed(mfhe, orc):
     """MFHE_OPT_NTT_FUSED (the one-launch XCD-L2 hand-off, r02-r03) was removed in r04: its hand-off was never
     proven (VERDICT r03 weak #6) and it was slower.  0 is still accepted; anything else fails loudly."""
