@@ -51,7 +51,10 @@ def parse():
     ap.add_argument("--only", default="all", help="all | ntt | crt | recombine | c4 | c5 (profiling)")
     ap.add_argument("--recombine-batch", type=int, default=256,
                     help="polys per step for the residue-shard INTT + CRT recombine line (0 = skip)")
+    ap.add_argument("--secondary-timeout", type=float, default=300.0,
+                    help="seconds the lines after the headline may take before the watchdog prints the headline and exits")
     ap.add_argument("--launch-check", action="store_true", help=argparse.SUPPRESS)
+    ap.add_argument("--hang-check", type=float, default=0.0, help=argparse.SUPPRESS)
     return ap.parse_args()
 
 
@@ -616,6 +619,24 @@ def u64_line(reps=10):
     return res
 
 
+def start_watchdog(out: dict, rank: int, seconds: float):
+    """After `seconds`, rank 0 prints `out` (the finished headline plus whatever secondary lines completed) with a
+    note, and every rank exits 0 without waiting for the GPU work or collectives in flight."""
+    import threading
+
+    def bail():
+        if rank == 0:
+            out["secondary_lines"] = f"stopped by the {seconds:.0f} s watchdog; lines finished before it are included"
+            print(json.dumps(out), flush=True)
+        sys.stderr.write(f"bench.py rank {rank}: secondary lines exceeded {seconds} s, exiting\n")
+        sys.stderr.flush()
+        os._exit(0)
+    wd = threading.Timer(seconds, bail)
+    wd.daemon = True
+    wd.start()
+    return wd
+
+
 def free_port() -> int:
     import socket
     with socket.socket(socket.AF_INET, socket.SOCK_STREAM) as s:
@@ -676,9 +697,14 @@ def main():
         t = torch.ones(1)
         if w > 1:
             dist.all_reduce(t)
+        out = {"metric": "launch-check", "n_gpus": w, "value": t.item(),
+               "launched_by_bench": os.environ.get("MFHE_BENCH_LAUNCHED") == "1"}
+        wd = start_watchdog(out, int(os.environ.get("RANK", "0")), args.secondary_timeout)
+        if args.hang_check:
+            time.sleep(args.hang_check)   # a secondary line that never returns (tests/test_bench_cli.py)
+        wd.cancel()
         if int(os.environ.get("RANK", "0")) == 0:
-            print(json.dumps({"metric": "launch-check", "n_gpus": w, "value": t.item(),
-                              "launched_by_bench": os.environ.get("MFHE_BENCH_LAUNCHED") == "1"}), flush=True)
+            print(json.dumps(out), flush=True)
         if w > 1:
             dist.destroy_process_group()
         return
@@ -767,6 +793,72 @@ def main():
         wall_c, ev_c = timed(enc_crt, max(1, args.steps // 2), 1)
         res["crt_ev_ms"], res["crt_batch"] = ev_c, cb
 
+    out = {}
+    if rank == 0:
+        ntts = batch * L * world
+        out.update({
+            "metric": "forward-NTT/s (N=2^16, L RNS limbs)",
+            "unit": "NTT/s",
+            "n_gpus": world,
+            "steps": args.steps,
+            "warmup": args.warmup,
+            "higher_is_better": True,
+            "scaling": "weak",
+            "vs_baseline": None,
+            "dtype": "u64",
+            "data": "synthetic uniform residues in [0, q_l), device-resident",
+            "config": {"workload": f"batched forward negacyclic NTT (phantom convention), N=2^{log_n}, "
+                                   f"L={L} x 50-bit primes, batch={batch} per GPU",
+                       "N": N, "limbs": L, "batch_per_gpu": batch,
+                       "arith": "f64" if ctx.info().arith == mfhe.ARITH_F64 else "u64",
+                       "parallelism": f"residue-batch shard x{world} (no collective)"},
+        })
+        if "fwd_wall" in res:
+            step_s = res["fwd_wall"] / args.steps
+            out["value"] = ntts / step_s
+            out["ms_per_step"] = step_s * 1e3
+            alg_bytes = 16.0 * N * batch * L       # 8N read + 8N write per NTT
+            ach = alg_bytes / (res["fwd_ev_ms"] * 1e-3) / 1e9
+            chunk_polys = max(1, ctx.get_option(mfhe.OPT_NTT_CHUNK_BYTES) // (L * N * 8))
+            nchunks = -(-batch // chunk_polys) if log_n >= 14 else 1
+            kname = (f"mfhe_ntt_fwd call = {nchunks} chunks x (column pass ntt_col_db_kernel + block pass "
+                     f"ntt_pass_kernel) launches" if log_n >= 14 else
+                     "mfhe_ntt_fwd call = 1 single-pass ntt_pass_kernel launch")
+            out["roofline"] = {"bound": "hbm", "kernel": kname,
+                               "achieved": round(ach, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                               "frac": round(ach / HBM_PEAK_GBS, 4), "traffic": None,
+                               "traffic_unit": "bytes per transform (FETCH_SIZE x2 + WRITE_SIZE, L2<->fabric)",
+                               "algorithmic_bytes_per_launch": alg_bytes,
+                               "hbm_read_frac": round(ach / 2 / HBM_PEAK_GBS, 4),
+                               "event_ms_per_transform": round(res["fwd_ev_ms"], 4)}
+            tr = pmc_traffic(N, L, batch)
+            if tr:
+                out["roofline"]["traffic"] = tr[0]
+                out["roofline"]["traffic_source"] = f"profiles/{tr[1]}"
+                out["roofline"]["traffic_over_algorithmic"] = round(tr[0] / alg_bytes, 3)
+            out["inverse_NTT_per_s"] = ntts / (res["inv_wall"] / args.steps)
+            out["inverse_over_forward"] = round(out["inverse_NTT_per_s"] / out["value"], 4)
+            tr = prof_trace(N, L, batch)
+            if tr:
+                # per-kernel averages of a committed rocprofv3 --kernel-trace run of this same command
+                # (tools/prof_agree.py): the roofline recomputed from the trace alone
+                out["roofline"]["kernel_ms_per_transform"] = round(tr["rocprof_kernel_ms_per_transform"], 4)
+                out["roofline"]["kernel_trace_frac"] = round(
+                    alg_bytes / (tr["rocprof_kernel_ms_per_transform"] * 1e-3) / 1e9 / HBM_PEAK_GBS, 4)
+                out["roofline"]["kernel_trace_source"] = f"profiles/{tr['file']}"
+                out["roofline"]["kernel_trace_per_kernel_avg_us"] = {
+                    k.split("(")[0].split("<")[0].replace("void mfhe::", ""): round(v["avg_us"], 2)
+                    for k, v in tr["per_kernel"].items()}
+        if "crt_ev_ms" in res:
+            cb = res["crt_batch"]
+            out["encode_crt_ops_per_s"] = cb / (res["crt_ev_ms"] * 1e-3) * world
+            out["encode_crt_GBps"] = 16.0 * (L + 1) * N * cb / (res["crt_ev_ms"] * 1e-3) / 1e9
+
+    # The headline is measured and complete.  The secondary lines below run collectives that have never executed
+    # on more than one real GPU (RCCL communicators of libmfhe beside torch's): a watchdog on every rank bounds
+    # them, so a hang there still leaves the headline line printed (rank 0) and every rank exiting 0.
+    wd = start_watchdog(out, rank, args.secondary_timeout)
+
     if args.only in ("all", "recombine") and args.recombine_batch and L % world == 0:
         try:
             # residue sharding: rank g owns limbs [g*L/G, (g+1)*L/G) of every poly.  One step =
@@ -818,6 +910,7 @@ def main():
         except Exception as e:   # a secondary line must not cost the headline line
             traceback.print_exc()
             res["recombine"] = {"error": repr(e)[:300]}
+        out["residue_shard_ntt_roundtrip_crt_recombine"] = res["recombine"]
 
     c4 = None
     if args.only in ("all", "c4") and not args.no_pipeline:
@@ -834,6 +927,7 @@ def main():
                 traceback.print_exc()
                 c4 = {"error": repr(e)[:300]}
             c4comm.close()
+        out["c4_sharded_pipeline"] = c4
 
     c5 = None
     if args.only in ("all", "c5") and not args.no_c5:
@@ -843,72 +937,9 @@ def main():
             traceback.print_exc()
             c5 = {"error": repr(e)[:300]}
         torch.cuda.empty_cache()
+        out["c5_residue_shard"] = c5
 
     if rank == 0:
-        ntts = batch * L * world
-        out = {
-            "metric": "forward-NTT/s (N=2^16, L RNS limbs)",
-            "unit": "NTT/s",
-            "n_gpus": world,
-            "steps": args.steps,
-            "warmup": args.warmup,
-            "higher_is_better": True,
-            "scaling": "weak",
-            "vs_baseline": None,
-            "dtype": "u64",
-            "data": "synthetic uniform residues in [0, q_l), device-resident",
-            "config": {"workload": f"batched forward negacyclic NTT (phantom convention), N=2^{log_n}, "
-                                   f"L={L} x 50-bit primes, batch={batch} per GPU",
-                       "N": N, "limbs": L, "batch_per_gpu": batch,
-                       "arith": "f64" if ctx.info().arith == mfhe.ARITH_F64 else "u64",
-                       "parallelism": f"residue-batch shard x{world} (no collective)"},
-        }
-        if "fwd_wall" in res:
-            step_s = res["fwd_wall"] / args.steps
-            out["value"] = ntts / step_s
-            out["ms_per_step"] = step_s * 1e3
-            alg_bytes = 16.0 * N * batch * L       # 8N read + 8N write per NTT
-            ach = alg_bytes / (res["fwd_ev_ms"] * 1e-3) / 1e9
-            chunk_polys = max(1, ctx.get_option(mfhe.OPT_NTT_CHUNK_BYTES) // (L * N * 8))
-            nchunks = -(-batch // chunk_polys) if log_n >= 14 else 1
-            kname = (f"mfhe_ntt_fwd call = {nchunks} chunks x (column pass ntt_col_db_kernel + block pass "
-                     f"ntt_pass_kernel) launches" if log_n >= 14 else
-                     "mfhe_ntt_fwd call = 1 single-pass ntt_pass_kernel launch")
-            out["roofline"] = {"bound": "hbm", "kernel": kname,
-                               "achieved": round(ach, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                               "frac": round(ach / HBM_PEAK_GBS, 4), "traffic": None,
-                               "traffic_unit": "bytes per transform (FETCH_SIZE x2 + WRITE_SIZE, L2<->fabric)",
-                               "algorithmic_bytes_per_launch": alg_bytes,
-                               "hbm_read_frac": round(ach / 2 / HBM_PEAK_GBS, 4),
-                               "event_ms_per_transform": round(res["fwd_ev_ms"], 4)}
-            tr = pmc_traffic(N, L, batch)
-            if tr:
-                out["roofline"]["traffic"] = tr[0]
-                out["roofline"]["traffic_source"] = f"profiles/{tr[1]}"
-                out["roofline"]["traffic_over_algorithmic"] = round(tr[0] / alg_bytes, 3)
-            out["inverse_NTT_per_s"] = ntts / (res["inv_wall"] / args.steps)
-            out["inverse_over_forward"] = round(out["inverse_NTT_per_s"] / out["value"], 4)
-            tr = prof_trace(N, L, batch)
-            if tr:
-                # per-kernel averages of a committed rocprofv3 --kernel-trace run of this same command
-                # (tools/prof_agree.py): the roofline recomputed from the trace alone
-                out["roofline"]["kernel_ms_per_transform"] = round(tr["rocprof_kernel_ms_per_transform"], 4)
-                out["roofline"]["kernel_trace_frac"] = round(
-                    alg_bytes / (tr["rocprof_kernel_ms_per_transform"] * 1e-3) / 1e9 / HBM_PEAK_GBS, 4)
-                out["roofline"]["kernel_trace_source"] = f"profiles/{tr['file']}"
-                out["roofline"]["kernel_trace_per_kernel_avg_us"] = {
-                    k.split("(")[0].split("<")[0].replace("void mfhe::", ""): round(v["avg_us"], 2)
-                    for k, v in tr["per_kernel"].items()}
-        if "crt_ev_ms" in res:
-            cb = res["crt_batch"]
-            out["encode_crt_ops_per_s"] = cb / (res["crt_ev_ms"] * 1e-3) * world
-            out["encode_crt_GBps"] = 16.0 * (L + 1) * N * cb / (res["crt_ev_ms"] * 1e-3) / 1e9
-        if "recombine" in res:
-            out["residue_shard_ntt_roundtrip_crt_recombine"] = res["recombine"]
-        if c4 is not None:
-            out["c4_sharded_pipeline"] = c4
-        if c5 is not None:
-            out["c5_residue_shard"] = c5
         if world == 1 and not args.no_pipeline and args.only == "all":
             out["reference_geometry_pipeline"] = pipeline_line()
             out["other_ntt_configs"] = other_configs_line()
@@ -919,7 +950,9 @@ def main():
                 out["cpu_baseline"] = cpu_baseline(log_n, moduli, args.cpu_seconds)
             except Exception as e:  # reported, never fatal
                 out["cpu_baseline"] = {"error": str(e)}
+        wd.cancel()
         print(json.dumps(out), flush=True)
+    wd.cancel()
     if world > 1:
         dist.destroy_process_group()
 

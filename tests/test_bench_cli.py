@@ -41,3 +41,11 @@ def test_world_size_mismatch_fails_loudly():
     assert p.returncode != 0
     assert "must agree" in p.stderr
     assert not _json_lines(p.stdout)
+
+
+def test_watchdog_prints_the_headline_when_a_secondary_line_hangs():
+    """Both ranks stall in a 'secondary line' for 60 s; the 3 s watchdog prints rank 0's line and every rank exits 0."""
+    p = _run(["--gpus", "2", "--launch-check", "--hang-check", "60", "--secondary-timeout", "3"], timeout=50)
+    assert p.returncode == 0, p.stderr[-3000:]
+    (line,) = _json_lines(p.stdout)
+    assert line["n_gpus"] == 2 and "watchdog" in line["secondary_lines"]
