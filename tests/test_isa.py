@@ -150,3 +150,28 @@ def test_wcrt_ring_gemm_no_one_ahead_instantiation_at_d6():
     for mode in (0, 1, 2):
         with pytest.raises(BaseException):
             _kernel_asm(r"_ZN4mfhe25mod_gemm_mfma_ring_kernelILi6ELi%dELb1E[^>]*" % mode)
+
+
+@pytest.mark.parametrize("inv", [0, 1], ids=["forward", "inverse"])
+def test_single_pass_14_has_no_memory_traffic_inside_the_transform(inv):
+    """ntt14_kernel (ntt_single14.hpp): the next polynomial's 16 loads per thread are issued before the transform
+    and must stay in flight through it, so between the loop's prefetch and its 16 stores there is no vector-memory
+    instruction (the twiddles come from LDS) and no scratch anywhere (the LICM-hoisted addresses once spilled 102
+    VGPRs).  Barriers are LDS-only: no `__syncthreads()` release fence (vmcnt(0)) between the loads and the stores."""
+    asm = _kernel_asm(r"_ZN4mfhe12ntt14_kernelILb%dEEEvNS_8PassArgsINS_6TwSrcFEEE" % inv)
+    lines = [ln.split("//")[0].strip() for ln in asm.split("\n") if ln.strip()]
+    ops = collections.Counter(re.findall(r"^\s+((?:global|buffer|flat|scratch)_[a-z0-9_]+)", asm, re.M))
+    assert not any(k.startswith("scratch_") for k in ops), ops
+    assert ops["buffer_load_dwordx2"] == 32 and ops["buffer_store_dwordx2"] == 16, ops
+    loads = [i for i, ln in enumerate(lines) if ln.startswith("buffer_load_dwordx2")]
+    stores = [i for i, ln in enumerate(lines) if ln.startswith("buffer_store_dwordx2")]
+    pf_end, st0 = loads[-1], stores[0]   # the in-loop prefetch is the second group of 16 loads
+    assert pf_end < st0
+    body = lines[pf_end + 1:st0]
+    assert not any(re.match(r"(global|buffer|flat)_", ln) for ln in body), "vector memory inside the transform"
+    assert sum(ln.startswith("s_barrier") for ln in body) >= 8, "the four exchanges' barriers"
+    # a vmcnt wait inside the transform waits for the prefetch: allowed only in the last exchange + store tail
+    # (the compiler's loop-carried register copies of the prefetched words), not before the third exchange
+    waits = [i for i, ln in enumerate(body) if "vmcnt" in ln]
+    bars = [i for i, ln in enumerate(body) if ln.startswith("s_barrier")]
+    assert not waits or min(waits) > bars[5], (waits[:3], bars)
