@@ -1025,18 +1025,24 @@ __global__ __launch_bounds__(256, D <= 5 ? 2 : 1) void mod_gemm_mfma_lds_kernel(
 }
 
 // Ring variant (MFHE_OPT_WCRT_PIPE 2 / 3, and 0 = auto on the factored launch): the same tile, digit planes and
-// epilogue, but the K loop runs over 32-k stages (one panel per digit plane per operand, 4 D KiB) held in a
-// 4-slot LDS ring (80 KiB at D = 5: still 2 workgroups per CU).  Stage s + 3 is DMA'd while stage s is
-// multiplied, so a stage's bytes have three stage times to land instead of one, and the wait at the end of
-// stage s is a counted vmcnt that leaves stages s + 2 and s + 3 in flight (D DMA instructions per thread per
-// stage; nothing else in the loop touches vector memory).  The barrier after it is a raw s_barrier
-// (__syncthreads' fence would wait for the DMAs in flight).  Slot (s + 3) & 3 = (s - 1) & 3 was last read in
-// stage s - 1, which every wave has left at that barrier.
+// epilogue, but the K loop runs over 32-k stages (one panel per digit plane per operand, 4 D KiB) held in an
+// NSLOT-slot LDS ring: stage s + NSLOT - 1 is DMA'd while stage s is multiplied, so a stage's bytes have NSLOT - 1
+// stage times to land instead of one, and the wait at the end of stage s is a counted vmcnt that leaves the later
+// stages in flight (D DMA instructions per thread per stage; nothing else in the loop touches vector memory).  The
+// barrier after it is a raw s_barrier (__syncthreads' fence would wait for the DMAs in flight).  Slot
+// (s + NSLOT - 1) % NSLOT = (s - 1) % NSLOT was last read in stage s - 1, which every wave has left at that barrier.
+// NSLOT = 4 at D = 5 (80 KiB, 2 workgroups per CU); 3 at D = 6 (72 KiB): with its registers held to 256 (launch
+// bounds) the D = 6 limb (the reference's 44-bit q0) also runs 2 workgroups per CU -- r03 ran it at 96 KiB and 384
+// VGPRs, one workgroup per CU and 0.22 MFMA busy (profiles/r03_gemm_sq_pmc.txt).
 // AHEAD: the next A fragment's LDS read is issued before the current fragment's D MFMAs (sched_barrier-pinned),
 // so its latency hides behind them instead of being waited for in front of them (D <= 5 only: at D >= 6 the
 // extra fragment spills).
+template <int D>
+constexpr int ring_slots() { return D <= 5 ? 4 : 3; }
+template <int D, int MODE>
+constexpr int ring_lds_bytes() { return ring_slots<D>() * 2 * D * 64 * 32; }
 template <int D, int MODE, bool AHEAD>
-__global__ __launch_bounds__(256, D <= 5 ? 2 : 1) void mod_gemm_mfma_ring_kernel(ModGemmArgs a, uint32_t Ppad, int limb0) {
+__device__ __forceinline__ void ring_tile(const ModGemmArgs& a, uint32_t Ppad, int l, int8_t* lds) {
     constexpr bool FAC = MODE != 0;
     constexpr int KK = FAC ? FK : MK, AM = FAC ? FK : 512;
     const uint32_t Pcols = FAC ? 2 * Ppad : Ppad;
@@ -1044,10 +1050,8 @@ __global__ __launch_bounds__(256, D <= 5 ? 2 : 1) void mod_gemm_mfma_ring_kernel
     constexpr int NST = KK / 32;                 // 32-k stages
     constexpr int PANEL = 64 * 32;               // 64 rows x 32 k of one digit plane (bytes)
     constexpr int STAGE = 2 * D * PANEL;         // A planes then B planes
-    constexpr int NSLOT = 4;
-    static_assert(NST >= NSLOT, "ring prologue assumes at least 4 stages");
-    __shared__ __attribute__((aligned(16))) int8_t lds[NSLOT * STAGE];
-    const int l = limb0 + blockIdx.z;
+    constexpr int NSLOT = ring_slots<D>(), LEAD = NSLOT - 1;
+    static_assert(NST >= NSLOT, "ring prologue assumes at least NSLOT stages");
     const int t = threadIdx.x, lane = t & 63, w = t >> 6;
     const int r = lane & 31, h = lane >> 5;
     const int mb = blockIdx.y * 64, pb = blockIdx.x * 64;
@@ -1060,7 +1064,7 @@ __global__ __launch_bounds__(256, D <= 5 ? 2 : 1) void mod_gemm_mfma_ring_kernel
     const uint64_t pstride = rows * KK, kstride = rows * 32;
     const int wbase = (ldA ? 0 : D * PANEL) + (li & ~63) * 16;
     auto issue = [&](int s) {
-        int8_t* dst = lds + (s & (NSLOT - 1)) * STAGE + wbase;
+        int8_t* dst = lds + (s % NSLOT) * STAGE + wbase;
 #pragma unroll
         for (int i = 0; i < D; ++i)
             __builtin_amdgcn_global_load_lds((const void*)(src + i * pstride + (uint64_t)s * kstride),
@@ -1071,14 +1075,14 @@ __global__ __launch_bounds__(256, D <= 5 ? 2 : 1) void mod_gemm_mfma_ring_kernel
     v16i acc[NS];
 #pragma unroll
     for (int s = 0; s < NS; ++s) acc[s] = v16i{0};
-    issue(0);
-    issue(1);
-    issue(2);
-    asm volatile("s_waitcnt vmcnt(%0)" ::"n"(2 * D) : "memory");   // stage 0 landed (1 and 2 in flight)
+#pragma unroll
+    for (int s = 0; s < LEAD; ++s) issue(s);
+    asm volatile("s_waitcnt vmcnt(%0)" ::"n"((LEAD - 1) * D) : "memory");   // stage 0 landed (1 .. LEAD - 1 in flight)
     barrier();
+#pragma unroll
     for (int s = 0; s < NST; ++s) {
-        if (s + 3 < NST) issue(s + 3);
-        const int8_t* st = lds + (s & (NSLOT - 1)) * STAGE;
+        if (s + LEAD < NST) issue(s + LEAD);
+        const int8_t* st = lds + (s % NSLOT) * STAGE;
         v4i bv[D];
 #pragma unroll
         for (int j = 0; j < D; ++j) bv[j] = *(const v4i*)(st + (D + j) * PANEL + (wp + r) * 32 + 16 * h);
@@ -1103,9 +1107,9 @@ __global__ __launch_bounds__(256, D <= 5 ? 2 : 1) void mod_gemm_mfma_ring_kernel
                     acc[i + j] = __builtin_amdgcn_mfma_i32_32x32x32_i8(av, bv[j], acc[i + j], 0, 0, 0);
             }
         }
-        // stage s + 1 landed for this wave: newer are the DMAs of stages s + 2 and s + 3 that were issued
+        // stage s + 1 landed for this wave: newer are the DMAs of the stages after it that were issued
         if (s + 1 < NST) {
-            const int newer = (s + 3 < NST ? s + 3 : NST - 1) - (s + 1);
+            const int newer = (s + LEAD < NST ? s + LEAD : NST - 1) - (s + 1);
             if (newer == 2) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(2 * D) : "memory");
             else if (newer == 1) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(D) : "memory");
             else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
@@ -1113,6 +1117,27 @@ __global__ __launch_bounds__(256, D <= 5 ? 2 : 1) void mod_gemm_mfma_ring_kernel
         }
     }
     mfma_epilogue<D, MODE>(a, acc, l, mb + wm, (uint32_t)(pb + wp), r, h, Ppad, icc);
+}
+
+template <int D, int MODE, bool AHEAD>
+__global__ __launch_bounds__(256, D <= 5 || (D == 6 && MODE != 0) ? 2 : 1)   // dense D = 6 spills at 256 VGPRs
+void mod_gemm_mfma_ring_kernel(ModGemmArgs a, uint32_t Ppad, int limb0) {
+    __shared__ __attribute__((aligned(16))) int8_t lds[ring_lds_bytes<D, MODE>()];
+    ring_tile<D, MODE, AHEAD>(a, Ppad, limb0 + (int)blockIdx.z, lds);
+}
+
+// r04: the factored launches' limbs at D = 5 and D = 6 in one grid (the reference's 44-bit q0 needs six
+// digits and ran as its own one-limb launch at 0.22 MFMA busy).  The digit count is per limb (bit l of d6, workgroup-
+// uniform: blockIdx.z), the two bodies share one LDS ring (max of 80 KiB at D = 5 and 72 KiB at D = 6) and one
+// register budget (<= 256: 2 workgroups per CU for both); limb 0's tiles dispatch first (z slowest), so the heavier
+// tiles do not form the tail.
+template <int MODE>
+__global__ __launch_bounds__(256, 2) void mod_gemm_mfma_ring56_kernel(ModGemmArgs a, uint32_t Ppad, int limb0, uint64_t d6) {
+    constexpr int B5 = ring_lds_bytes<5, MODE>(), B6 = ring_lds_bytes<6, MODE>();
+    __shared__ __attribute__((aligned(16))) int8_t lds[B5 > B6 ? B5 : B6];
+    const int l = limb0 + (int)blockIdx.z;
+    if ((d6 >> blockIdx.z) & 1) ring_tile<6, MODE, false>(a, Ppad, l, lds);
+    else ring_tile<5, MODE, false>(a, Ppad, l, lds);
 }
 
 // The ring kernel's waits are counted (vmcnt(D) / vmcnt(2D): the DMAs of the stages still in flight).  A build in
@@ -1129,6 +1154,33 @@ static bool ring_usable() {
              fa.localSizeBytes == 0;
     }
     return ok == 1;
+}
+
+template <int MODE>
+static bool ring56_usable() {
+    static int ok = -1;
+    if (ok < 0) {
+        hipFuncAttributes fa{};
+        ok = hipFuncGetAttributes(&fa, reinterpret_cast<const void*>(mod_gemm_mfma_ring56_kernel<MODE>)) == hipSuccess &&
+             fa.localSizeBytes == 0;
+    }
+    return ok == 1;
+}
+
+// factored launches, pipe 0 (auto): every limb at D = 5 or 6 in one ring56 grid.  Returns false (nothing launched)
+// when that does not apply: another pipe, a digit count outside {5, 6}, more than 64 limbs, or a spilling build.
+template <int MODE>
+static bool launch_ring56(const ModGemmArgs& f, int L, uint32_t Ppad, hipStream_t s) {
+    if (f.pipe != 0 || L > 64 || !ring56_usable<MODE>()) return false;
+    uint64_t d6 = 0;
+    for (int l = 0; l < L; ++l) {
+        const int d = f.limbD ? std::max(f.limbD[l], 5) : f.D;
+        if (d != 5 && d != 6) return false;
+        if (d == 6) d6 |= 1ull << l;
+    }
+    const dim3 grid(2 * Ppad / 64, FK / 64, L);
+    hipLaunchKernelGGL((mod_gemm_mfma_ring56_kernel<MODE>), grid, dim3(256), 0, s, f, Ppad, 0, d6);
+    return true;
 }
 
 // pipe: 1 = two-stage LDS kernel; 3 = ring + one-ahead A read (D <= 5); anything else = ring
@@ -1196,6 +1248,10 @@ static int launch_factored(const ModGemmArgs& a, int L, hipStream_t s) {
                            Ppad, a.fold, a.Bdig, f.d0, pc);
     }
     MFHE_CHECK_LAUNCH("mfma_digitize_fold_kernel");
+    if (launch_ring56<1>(f, L, Ppad, s)) {
+        MFHE_CHECK_LAUNCH("mod_gemm_mfma_ring56_kernel (factored)");
+        return MFHE_OK;
+    }
     for (int l0 = 0; l0 < L;) {
         const int d = a.limbD ? std::max(a.limbD[l0], 5) : a.D;
         int l1 = l0 + 1;
@@ -1221,6 +1277,10 @@ static int launch_factored_inv(const ModGemmArgs& a, int L, hipStream_t s) {
     if (a.D == 5) hipLaunchKernelGGL(mfma_digitize_ifold_kernel<5>, gd, dim3(256), 0, s, f, Ppad, pc);
     else hipLaunchKernelGGL(mfma_digitize_ifold_kernel<6>, gd, dim3(256), 0, s, f, Ppad, pc);
     MFHE_CHECK_LAUNCH("mfma_digitize_ifold_kernel");
+    if (launch_ring56<2>(f, L, Ppad, s)) {
+        MFHE_CHECK_LAUNCH("mod_gemm_mfma_ring56_kernel (factored inverse)");
+        return MFHE_OK;
+    }
     for (int l0 = 0; l0 < L;) {
         const int d = a.limbD ? std::max(a.limbD[l0], 5) : a.D;
         int l1 = l0 + 1;

@@ -98,6 +98,20 @@ struct ArithF64 {
     }
 };
 
+// hi64(a * b) with four multiplies and two glue instructions.  hi64 = ah bh + floor(S / 2^32), S = al bh + ah bl +
+// hi32(al bl) < 2^65: A = al bh + hi32(al bl) cannot overflow, the second middle product is accumulated by
+// v_mad_u64_u32 with its carry-out (an SGPR lane mask), and (carry, B >> 32) is the pair the last multiply adds.
+// __umul64hi's lowering re-pairs each 32-bit half with a zero register instead: 3-4 v_mov per call (tools/isa_mix.py).
+__device__ __forceinline__ uint64_t mulhi64(uint64_t a, uint64_t b) {
+    const uint32_t al = (uint32_t)a, ah = (uint32_t)(a >> 32), bl = (uint32_t)b, bh = (uint32_t)(b >> 32);
+    const uint64_t A = (uint64_t)al * bh + __umulhi(al, bl);
+    uint64_t B, c;
+    asm("v_mad_u64_u32 %0, %1, %2, %3, %4" : "=v"(B), "=s"(c) : "v"(ah), "v"(bl), "v"(A));
+    uint32_t ci;
+    asm("v_cndmask_b32 %0, 0, 1, %1" : "=v"(ci) : "s"(c));
+    return (uint64_t)ah * bh + (((uint64_t)ci << 32) | (uint32_t)(B >> 32));
+}
+
 struct ArithU64 {
     using T = uint64_t;
     using Tw = ulonglong2;   // (w, floor(w 2^64 / q))
@@ -131,7 +145,7 @@ struct ArithU64 {
     }
     // Shoup: v*w + hi64(v*w')*(-q) in [0,2q) for any v < 2^64
     __device__ __forceinline__ uint64_t mulmod(uint64_t v, Tw w) const {
-        return v * w.x + __umul64hi(v, w.y) * nq;
+        return v * w.x + mulhi64(v, w.y) * nq;
     }
     __device__ __forceinline__ uint64_t reduce(uint64_t x) const {   // [0,4q) -> [0,2q)
         return sel_sub(x, x + n2q);

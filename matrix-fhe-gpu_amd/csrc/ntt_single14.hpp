@@ -31,7 +31,8 @@
 #include "ntt_coldb.hpp"
 
 #ifndef MFHE_S14_EXP
-#define MFHE_S14_EXP 0   // timing probes (wrong results), never in the product build
+#define MFHE_S14_EXP 0   // timing probes (wrong results), never in the product build: 1 compute only, 2 exchanges +
+                         // memory, 3 memory only, 4 no stores, 5 no loads after the first
 #endif
 
 namespace mfhe {
@@ -45,13 +46,13 @@ struct S14 {
 // LDS slot of element j.  h XORs b5, b6, b7, b8 into bits 0, 2, 3, {1, 4}: every exchange access (ds_write_b64:
 // 16-lane groups must hit distinct slots mod 16; ds_read_b64: 32-lane groups, distinct mod 32) is conflict-free
 // in all four layouts (checked by tests/test_ntt14_layout.py).
-__device__ __host__ __forceinline__ uint32_t s14_swz(uint32_t j) {
+__device__ __host__ __forceinline__ constexpr uint32_t s14_swz(uint32_t j) {
     const uint32_t h = ((j >> 5) & 1u) | (((j >> 6) & 1u) << 2) | (((j >> 7) & 1u) << 3) | (((j >> 8) & 1u) * 18u);
     return j ^ h;
 }
 
 template <int LAY>
-__device__ __host__ __forceinline__ uint32_t s14_j(uint32_t t, uint32_t k) {
+__device__ __host__ __forceinline__ constexpr uint32_t s14_j(uint32_t t, uint32_t k) {
     const uint32_t lane = t & 63u, wave = t >> 6;
     if constexpr (LAY == 0) return (k << 10) | t;
     else if constexpr (LAY == 1) return (wave << 10) | (k << 6) | lane;
@@ -70,23 +71,68 @@ __device__ __forceinline__ uint32_t s14_opaque(uint32_t t) {
     return t;
 }
 
-template <int FROM, int TO>
-__device__ __forceinline__ void s14_exchange(double (&x)[16], double* lds, uint32_t t_) {
-    const uint32_t t = s14_opaque(t_);
-    lds_barrier();   // the previous readers of the buffer are done
-#pragma unroll
-    for (int k = 0; k < 16; ++k) lds[s14_swz(s14_j<FROM>(t, (uint32_t)k))] = x[k];
-    lds_barrier();
-#pragma unroll
-    for (int k = 0; k < 16; ++k) x[k] = lds[s14_swz(s14_j<TO>(t, (uint32_t)k))];
+// Exchange addressing.  j(t, k) = jt(t) | jk(k) with disjoint bits and the swizzle is XOR-linear, so
+// swz(j) = S(t) ^ C(k), S(t) = swz(jt(t)), C(k) = swz(jk(k)) a compile-time constant.  The bits of C outside those S
+// can occupy (TB: jt's bits and the swizzle's target bits 0..4) are added, which the ds_read / ds_write immediate
+// offset absorbs; only C & TB needs a v_xor (none in L0, 7 distinct in L1, 15 in L2 and L3).  One S per access group
+// instead of a full address computation per element (r04: ~500 -> ~110 VALU address instructions per polynomial).
+template <int LAY>
+__device__ __host__ constexpr uint32_t s14_tbits() {
+    uint32_t m = 0x1Fu;
+    for (uint32_t t = 0; t < 1024; ++t) m |= s14_j<LAY>(t, 0);
+    return m;
+}
+// In bytes, on the LDS address space: S8 = lds + 8 S once per access group, then one v_xor per element (the buffer is
+// 256-B aligned, so the XOR of bits 3..7 commutes with the base) and the added part in the instruction's offset.
+typedef __attribute__((address_space(3))) double lds_f64;
+__device__ __forceinline__ uint32_t s14_lds_addr(const double* p) { return (uint32_t)(size_t)(const lds_f64*)p; }
+template <int LAY, int K>
+__device__ __forceinline__ lds_f64* s14_slot(uint32_t S8) {
+    constexpr uint32_t c = s14_swz(s14_j<LAY>(0, (uint32_t)K)), tb = s14_tbits<LAY>();
+    static_assert(((c & tb) << 3) < 256, "XOR part stays inside the buffer's 256-B alignment");
+    return (lds_f64*)(size_t)((S8 ^ ((c & tb) << 3)) + ((c & ~tb) << 3));
+}
+template <int LAY>
+__device__ __forceinline__ uint32_t s14_s8(const double* lds, uint32_t t_) {
+    return s14_lds_addr(lds) + (s14_swz(s14_j<LAY>(s14_opaque(t_), 0)) << 3);
+}
+template <int LAY>
+__device__ __forceinline__ void s14_write(const double (&x)[16], double* lds, uint32_t t) {
+    const uint32_t S8 = s14_s8<LAY>(lds, t);
+    static_for<0, 16>([&](auto kc) { *s14_slot<LAY, decltype(kc)::value>(S8) = x[decltype(kc)::value]; });
+}
+template <int LAY>
+__device__ __forceinline__ void s14_read(double (&x)[16], double* lds, uint32_t t) {
+    const uint32_t S8 = s14_s8<LAY>(lds, t);
+    static_for<0, 16>([&](auto kc) { x[decltype(kc)::value] = *s14_slot<LAY, decltype(kc)::value>(S8); });
 }
 
-// Twiddle of stage s for the butterfly group whose lower element is j (index 2^s + (j >> (14 - s))), from the LDS
-// tables: direct below 2048, else the product of tab[idx & 2047] and btab[idx >> 11] = tw[idx & ~2047].
-__device__ __forceinline__ double s14_tw(const ArithF64& ar, const double* tab, const double* btab, int s, uint32_t j) {
-    const uint32_t idx = (1u << s) + (j >> (14 - s));
-    if (s <= 10) return tab[idx];
-    return ar.mulmod(tab[idx & 2047u], btab[idx >> 11]);
+// Exchange FROM -> TO.  L1, L2 and L3 keep each wave on its own 1024-element block (j >> 10 = wave), so an exchange
+// between two of them is wave-local: the wave reads only slots it wrote, LDS operations of one wave are performed in
+// order, and no other wave touches that block between the cross-wave exchanges -- a wait for this wave's own writes
+// suffices, no s_barrier.  L0 spreads every thread over all 16 blocks: writing it needs every wave to be done with
+// the buffer's previous image (barrier before), reading it needs every wave's writes (barrier after the writes).
+// Writing L1..L3 needs no barrier before (only this wave reads its block since the last cross-wave exchange).
+template <int FROM, int TO>
+__device__ __forceinline__ void s14_exchange(double (&x)[16], double* lds, uint32_t t) {
+    if constexpr (FROM == 0) lds_barrier();   // the previous readers of the buffer are done
+    s14_write<FROM>(x, lds, t);
+    if constexpr (FROM == 0 || TO == 0) lds_barrier();
+    else asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    s14_read<TO>(x, lds, t);
+}
+
+// Twiddle of stage S for the butterfly group whose lower element is j = jt | JK (thread part, compile-time register
+// part; disjoint bits): index 2^S + (j >> (14 - S)), from the LDS tables -- direct below 2048, else the product of
+// tab[idx & 2047] and btab[idx >> 11] = tw[idx & ~2047].  The shifted parts stay disjoint, so the register part is an
+// added constant (the ds_read offset) and the thread part one VGPR per stage.
+template <int S, uint32_t JK>
+__device__ __forceinline__ double s14_tw(const ArithF64& ar, const double* tab, const double* btab, uint32_t jt) {
+    constexpr int sh = 14 - S;
+    constexpr uint32_t ck = (1u << S) | (JK >> sh);
+    const uint32_t vt = jt >> sh;
+    if constexpr (S <= 10) return tab[vt + ck];
+    else return ar.mulmod(tab[(vt & 2047u) + (ck & 2047u)], btab[(vt >> 11) + (ck >> 11)]);
 }
 
 // CT stages on register bits BB_HI .. BB_LO (descending) of layout LAY
@@ -99,8 +145,11 @@ __device__ __forceinline__ void s14_ct_round(double (&x)[16], const ArithF64& ar
         constexpr int b = s14_kbase<LAY>() + bb, s = 13 - b, half = 1 << bb;
         // one twiddle per group of butterflies sharing the register bits above bb
         double w[16 >> (bb + 1)];
-#pragma unroll
-        for (int g = 0; g < (16 >> (bb + 1)); ++g) w[g] = s14_tw(ar, tab, btab, s, s14_j<LAY>(t, (uint32_t)(g << (bb + 1))));
+        const uint32_t jt = s14_j<LAY>(t, 0);
+        static_for<0, (16 >> (bb + 1))>([&](auto gc) {
+            constexpr int g = decltype(gc)::value;
+            w[g] = s14_tw<s, s14_j<LAY>(0, (uint32_t)(g << (bb + 1)))>(ar, tab, btab, jt);
+        });
 #pragma unroll
         for (int k = 0; k < 16; ++k) {
             if (k & half) continue;
@@ -129,9 +178,11 @@ __device__ __forceinline__ void s14_gs_round(double (&x)[16], const ArithF64& ar
             }
         } else {
             double w[16 >> (bb + 1)];
-#pragma unroll
-            for (int g = 0; g < (16 >> (bb + 1)); ++g)
-                w[g] = s14_tw(ar, tab, btab, s, s14_j<LAY>(t, (uint32_t)(g << (bb + 1))));
+            const uint32_t jt = s14_j<LAY>(t, 0);
+            static_for<0, (16 >> (bb + 1))>([&](auto gc) {
+                constexpr int g = decltype(gc)::value;
+                w[g] = s14_tw<s, s14_j<LAY>(0, (uint32_t)(g << (bb + 1)))>(ar, tab, btab, jt);
+            });
 #pragma unroll
             for (int k = 0; k < 16; ++k) {
                 if (k & half) continue;
@@ -144,7 +195,7 @@ __device__ __forceinline__ void s14_gs_round(double (&x)[16], const ArithF64& ar
 
 template <bool INV>
 __global__ __launch_bounds__(S14::NT, 1) void ntt14_kernel(PassArgs<TwSrcF> a) {
-    extern __shared__ __attribute__((aligned(16))) uint64_t lds_raw[];
+    extern __shared__ __attribute__((aligned(256))) uint64_t lds_raw[];   // 256: s14_slot's XOR
     double* lds = (double*)lds_raw;
     double* tab = lds + S14::N;          // [2048]: tw[0, 2048) of the limb (inverse: itw, entry 1 without n^-1)
     double* btab = tab + S14::TAB;       // [8]: tw[2048 i]
@@ -211,11 +262,11 @@ __global__ __launch_bounds__(S14::NT, 1) void ntt14_kernel(PassArgs<TwSrcF> a) {
         int nmod = mod;
         if (more) {
             nbase = poly(nlt, &nmod);
-#if MFHE_S14_EXP != 1
+#if MFHE_S14_EXP != 1 && MFHE_S14_EXP != 5
             load(nbase, raw);   // in flight through the whole transform below
 #endif
         }
-#if MFHE_S14_EXP >= 2   // timing probes only (wrong results): 2 = no butterflies, 3 = no butterflies, no exchanges
+#if MFHE_S14_EXP == 2 || MFHE_S14_EXP == 3   // timing probes only (wrong results): 2 = no butterflies, 3 = no butterflies, no exchanges
         if (true) {
 #if MFHE_S14_EXP == 2
             s14_exchange<0, 1>(x, lds, t);
@@ -250,7 +301,7 @@ __global__ __launch_bounds__(S14::NT, 1) void ntt14_kernel(PassArgs<TwSrcF> a) {
             s14_exchange<1, 0>(x, lds, t);
             s14_gs_round<0, 0, 3>(x, ar, tab, btab, w1, ninv, t);
         }
-#if MFHE_S14_EXP == 1   // timing probe only: compute without memory traffic (loads once, never stores)
+#if MFHE_S14_EXP == 1 || MFHE_S14_EXP == 4   // timing probes only: no stores
         if (lt == 0xFFFFFFFFu)
 #endif
         {

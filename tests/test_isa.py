@@ -10,6 +10,7 @@ instruction mix and wait immediates; the library also refuses the kernel at run 
 """
 import collections
 import functools
+import os
 import re
 import subprocess
 import tempfile
@@ -18,7 +19,7 @@ from pathlib import Path
 import pytest
 
 ROOT = Path(__file__).resolve().parent.parent
-LIB = ROOT / "matrix-fhe-gpu_amd" / "libmfhe.so"
+LIB = ROOT / "matrix-fhe-gpu_amd" / os.environ.get("MFHE_ISA_LIB", "libmfhe.so")
 LLVM = Path("/opt/rocm/lib/llvm/bin")
 MAGIC = b"__CLANG_OFFLOAD_BUNDLE__"
 
@@ -124,8 +125,9 @@ def test_digitize_loads_are_not_serialised(kernel):
 @pytest.mark.parametrize("D,mode", [(5, 1), (6, 1), (5, 2), (6, 2)])
 def test_wcrt_ring_gemm_counted_waits(D, mode):
     """mod_gemm_mfma_ring_kernel<D, MODE, false> (gemm.hip), the default factored forward (MODE 1) and inverse
-    (MODE 2) W-CRT GEMM: its K loop waits for stage s with a counted `s_waitcnt vmcnt(D)` / `vmcnt(2D)` that leaves
-    the next stages' D DMA instructions each in flight.  Pinned: D DMAs per 32-k stage (K = 256: 8
+    (MODE 2) W-CRT GEMM: its K loop waits for stage s with a counted `s_waitcnt vmcnt(D)` / `vmcnt(2D)` (D = 5, four
+    ring slots) or `vmcnt(D)` (D = 6, three slots) that leaves the next stages' D DMA instructions each in flight
+    (ADVICE r03).  Pinned: D DMAs per 32-k stage (K = 256: 8
     stages, fully unrolled), no scratch traffic, no store and at most one other vector load between the first DMA
     and the last barrier of the K loop (an extra op issued there can only make a counted wait stricter), and only
     the immediates 0, D and 2D there.  The library also refuses a spilling ring kernel at run time (ring_usable)."""
@@ -141,8 +143,40 @@ def test_wcrt_ring_gemm_counted_waits(D, mode):
     assert not any("store" in ln or "atomic" in ln for ln in other), other
     assert len(other) <= 1, other
     waits = {int(v) for ln in region for v in re.findall(r"vmcnt\((\d+)\)", ln)}
-    assert waits <= {0, D, 2 * D} and {D, 2 * D} <= waits, waits
+    # ring_slots: 4 slots (stages s + 1 .. s + 3 in flight) at D = 5, 3 slots (s + 1, s + 2) at D = 6
+    want = {0, D, 2 * D} if D <= 5 else {0, D}
+    assert waits <= want and want - {0} <= waits, waits
     assert len(bar) == 8, len(bar)   # one barrier per stage: the prologue's and seven in the loop
+
+
+@pytest.mark.parametrize("mode", [1, 2])
+def test_wcrt_ring56_gemm_counted_waits(mode):
+    """mod_gemm_mfma_ring56_kernel<MODE> (gemm.hip, r04): the factored launch's D = 5 and D = 6 limbs in one grid, the
+    two ring bodies behind a workgroup-uniform branch.  Each body keeps its own counted waits (D = 5: vmcnt 0 / 5 / 10,
+    D = 6: 0 / 6), so the kernel holds 8 x (5 + 6) DMAs, 16 barriers, no scratch, no store and at most one other
+    vector load per body inside the K loops, and 2 workgroups per CU worth of registers (<= 256 VGPRs)."""
+    asm = _kernel_asm(r"_ZN4mfhe27mod_gemm_mfma_ring56_kernelILi%dEEEvNS_11ModGemmArgsEjim" % mode)
+    lines = asm.split("\n")
+    ops = collections.Counter(re.findall(r"^\s+((?:global|buffer|flat|scratch)_[a-z0-9_]+)", asm, re.M))
+    assert not any(k.startswith("scratch_") for k in ops), ops
+    bar = [i for i, ln in enumerate(lines) if "s_barrier" in ln]
+    assert len(bar) == 16, len(bar)
+    # the two bodies are laid out one after the other: each holds 8 barriers (prologue + 7 in its K loop)
+    seen = set()
+    for seg in (lines[:bar[7] + 1], lines[bar[7] + 1:]):
+        dma = [i for i, ln in enumerate(seg) if "global_load_lds_dwordx4" in ln]
+        D = len(dma) // 8
+        assert len(dma) == 8 * D and D in (5, 6), len(dma)
+        seen.add(D)
+        sbar = [i for i, ln in enumerate(seg) if "s_barrier" in ln]
+        region = seg[dma[0]:sbar[-1] + 1]
+        waits = {int(v) for ln in region for v in re.findall(r"vmcnt\((\d+)\)", ln)}
+        want = {0, D, 2 * D} if D == 5 else {0, D}
+        assert waits <= want and want - {0} <= waits, (D, waits)
+        other = [ln for ln in region if re.search(r"\b(global|buffer|flat)_", ln) and "global_load_lds" not in ln]
+        assert not any("store" in ln or "atomic" in ln for ln in other), other
+        assert len(other) <= 1, other
+    assert seen == {5, 6}, seen
 
 
 def test_wcrt_ring_gemm_no_one_ahead_instantiation_at_d6():
@@ -157,7 +191,8 @@ def test_single_pass_14_has_no_memory_traffic_inside_the_transform(inv):
     """ntt14_kernel (ntt_single14.hpp): the next polynomial's 16 loads per thread are issued before the transform
     and must stay in flight through it, so between the loop's prefetch and its 16 stores there is no vector-memory
     instruction (the twiddles come from LDS) and no scratch anywhere (the LICM-hoisted addresses once spilled 102
-    VGPRs).  Barriers are LDS-only: no `__syncthreads()` release fence (vmcnt(0)) between the loads and the stores."""
+    VGPRs).  Barriers are LDS-only: no `__syncthreads()` release fence (vmcnt(0)) between the loads and the stores,
+    and three per polynomial (the wave-local exchanges L1 <-> L2 <-> L3 have none)."""
     asm = _kernel_asm(r"_ZN4mfhe12ntt14_kernelILb%dEEEvNS_8PassArgsINS_6TwSrcFEEE" % inv)
     lines = [ln.split("//")[0].strip() for ln in asm.split("\n") if ln.strip()]
     ops = collections.Counter(re.findall(r"^\s+((?:global|buffer|flat|scratch)_[a-z0-9_]+)", asm, re.M))
@@ -169,9 +204,12 @@ def test_single_pass_14_has_no_memory_traffic_inside_the_transform(inv):
     assert pf_end < st0
     body = lines[pf_end + 1:st0]
     assert not any(re.match(r"(global|buffer|flat)_", ln) for ln in body), "vector memory inside the transform"
-    assert sum(ln.startswith("s_barrier") for ln in body) >= 8, "the four exchanges' barriers"
-    # a vmcnt wait inside the transform waits for the prefetch: allowed only in the last exchange + store tail
-    # (the compiler's loop-carried register copies of the prefetched words), not before the third exchange
-    waits = [i for i, ln in enumerate(body) if "vmcnt" in ln]
+    # r04: only the two cross-wave exchanges (L0 <-> L1 / L3) synchronise the workgroup -- one barrier before the L0
+    # image is written, one after it, one after the last wave-local image -- the wave-local ones wait for their
+    # own LDS writes only (lgkmcnt)
     bars = [i for i, ln in enumerate(body) if ln.startswith("s_barrier")]
-    assert not waits or min(waits) > bars[5], (waits[:3], bars)
+    assert len(bars) == 3, bars
+    # a vmcnt wait inside the transform waits for the prefetch: allowed only after the last barrier (the compiler's
+    # loop-carried register copies of the prefetched words), never inside the butterflies
+    waits = [i for i, ln in enumerate(body) if "vmcnt" in ln]
+    assert not waits or min(waits) > bars[-1], (waits[:3], bars)

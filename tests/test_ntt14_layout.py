@@ -71,3 +71,43 @@ def test_twiddle_product_rule(orc):
     tw = [pow(psi, brev(k), q) for k in range(1 << 14)]
     for k in list(range(2048, 1 << 14, 37)) + [2048, 4096, 8191, 16383]:
         assert tw[k] == tw[k & 2047] * tw[k & ~2047] % q, k
+
+
+def tbits(lay):
+    m = 0x1F
+    for t in range(1024):
+        m |= jidx(lay, t, 0)
+    return m
+
+
+def test_exchange_addresses_split_into_thread_xor_and_immediate():
+    """s14_slot: swz(j(t, k)) == (S(t) ^ (C(k) & TB)) + (C(k) & ~TB) with S(t) = swz(j(t, 0)), C(k) = swz(j(0, k));
+    the XOR part (in bytes) stays below the buffer's 256-B alignment; L1..L3 keep every wave on its own 1024-element
+    block (the wave-local exchanges need no s_barrier)."""
+    for lay in range(4):
+        tb = tbits(lay)
+        S = swz(jidx(lay, T, 0))
+        for k in range(16):
+            c = int(swz(jidx(lay, 0, k)))
+            assert ((c & tb) << 3) < 256, (lay, k)
+            assert np.array_equal((S ^ (c & tb)) + (c & ~tb), swz(jidx(lay, T, k))), (lay, k)
+            if lay:
+                assert np.array_equal(swz(jidx(lay, T, k)) >> 10, T >> 6), (lay, k)
+
+
+def test_twiddle_index_split():
+    """s14_tw: 2^s + (j >> (14 - s)) == 2^s | (jk >> sh) | (jt >> sh) with disjoint parts, so the & 2047 / >> 11 split
+    of stages 11..13 distributes over the two parts."""
+    for lay in range(4):
+        jt = jidx(lay, T, 0)
+        for s in range(14):
+            sh = 14 - s
+            for k in range(16):
+                jk = int(jidx(lay, 0, k))
+                ck = (1 << s) | (jk >> sh)
+                vt = jt >> sh
+                assert not np.any(vt & ck)
+                idx = (1 << s) + (jidx(lay, T, k) >> sh)
+                assert np.array_equal(idx, vt + ck)
+                assert np.array_equal(idx & 2047, (vt & 2047) + (ck & 2047))
+                assert np.array_equal(idx >> 11, (vt >> 11) + (ck >> 11))
