@@ -151,9 +151,17 @@ def other_configs_line(reps=10):
         del qt
 
         def rate(fn, nb):
-            for k in range(nb):
-                fn(bufs[k], batch=batch, start_limb=0, nlimbs=lg)
-            torch.cuda.synchronize()
+            # warm up for >= 50 ms of calls, not a fixed count: the clock ramps over the first ~30 ms of work
+            # (profiles/r02_bench_steps.txt), which a C2 call (~80 us) would otherwise spend inside the timed loop
+            t_end = time.perf_counter() + 0.05
+            k = 0
+            while True:
+                fn(bufs[k % nb], batch=batch, start_limb=0, nlimbs=lg)
+                k += 1
+                if k % nb == 0:
+                    torch.cuda.synchronize()
+                    if time.perf_counter() >= t_end:
+                        break
             e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
             e0.record()
             n = reps * nb

@@ -22,14 +22,18 @@
 //   L1: k -> b9..b6, lane -> b5..b0, wave -> b13..b10
 //   L2: k -> b5..b2, lane -> b1 b0 (lane bits 0, 1), b9..b6 (lane bits 2..5), wave -> b13..b10
 //   L3: k -> b3..b0, lane bits 0..3 -> b8..b5, lane bit 4 -> b4, lane bit 5 -> b9, wave -> b13..b10
-// Forward (CT, stage s pairs bit 13 - s): L0 stages 0-3 | L1 4-7 | L2 8-10 (b2 rides along) | L3 11-13 | -> L0.
-// Inverse (GS): L0 -> L3 stages 13-11 | L2 10-8 | L1 7-4 | L0 3-0 (n^-1 at s = 0).
+// Forward (CT, stage s pairs bit 13 - s): load L0, stages 0-3 | L1 4-7 | L2 8-10 (b2 rides along) | L3 11-13 | -> L1,
+// store.  Inverse (GS): load L1 -> L3 stages 13-11 | L2 10-8 | L1 7-4 | L0 3-0 (n^-1 at s = 0), store.  Only L0 is
+// cross-wave: two workgroup barriers per polynomial (r04), the other exchanges are wave-local.
 // Arithmetic and reduction schedule as in NttPass (ntt_arith.hpp): forward, one centred reduction at the start of
 // every round after the first (rounds of <= 4 stages: |x| < 3q); inverse, lazy GS on every other stage.
 // Reference: phantom fnwt_1d / inwt_1d per polynomial (ntt_core.cu:443-460); same outputs, bit for bit.
 #pragma once
 #include "ntt_coldb.hpp"
 
+#ifndef MFHE_S14_CPOL_OUT
+#define MFHE_S14_CPOL_OUT MFHE_NTT_CPOL_OUT   // output store policy (gfx950 CPol bits: 1 sc0, 2 nt, 16 sc1)
+#endif
 #ifndef MFHE_S14_EXP
 #define MFHE_S14_EXP 0   // timing probes (wrong results), never in the product build: 1 compute only, 2 exchanges +
                          // memory, 3 memory only, 4 no stores, 5 no loads after the first
@@ -109,13 +113,14 @@ __device__ __forceinline__ void s14_read(double (&x)[16], double* lds, uint32_t 
 
 // Exchange FROM -> TO.  L1, L2 and L3 keep each wave on its own 1024-element block (j >> 10 = wave), so an exchange
 // between two of them is wave-local: the wave reads only slots it wrote, LDS operations of one wave are performed in
-// order, and no other wave touches that block between the cross-wave exchanges -- a wait for this wave's own writes
-// suffices, no s_barrier.  L0 spreads every thread over all 16 blocks: writing it needs every wave to be done with
-// the buffer's previous image (barrier before), reading it needs every wave's writes (barrier after the writes).
-// Writing L1..L3 needs no barrier before (only this wave reads its block since the last cross-wave exchange).
-template <int FROM, int TO>
+// order -- a wait for this wave's own writes suffices, no s_barrier.  L0 spreads every thread over all 16 blocks:
+// reading it needs every wave's writes (barrier after the writes).  BAR: a barrier before the writes, needed by the
+// first exchange of a polynomial -- its writes land in blocks another wave may still be reading (the previous
+// polynomial's last exchange); inside a polynomial only the wave itself touches its block between the cross-wave
+// exchanges.
+template <int FROM, int TO, bool BAR>
 __device__ __forceinline__ void s14_exchange(double (&x)[16], double* lds, uint32_t t) {
-    if constexpr (FROM == 0) lds_barrier();   // the previous readers of the buffer are done
+    if constexpr (BAR) lds_barrier();   // the previous readers of the buffer are done
     s14_write<FROM>(x, lds, t);
     if constexpr (FROM == 0 || TO == 0) lds_barrier();
     else asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
@@ -214,11 +219,16 @@ __global__ __launch_bounds__(S14::NT, 1) void ntt14_kernel(PassArgs<TwSrcF> a) {
         return (uint64_t*)(((uint64_t)(uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)(pu >> 32)) << 32) |
                            (uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)pu));
     };
+    // global layouts: the forward loads L0 (its first round pairs b13..b10) and stores L1, the inverse loads L1 and
+    // stores L0; in both, each register's 64 lanes cover 512 contiguous bytes
+    constexpr int LIN = INV ? 1 : 0, LOUT = INV ? 0 : 1;
     auto load = [&](const uint64_t* base, uint64_t (&raw)[16]) {
         const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc((void*)base, 0, 0x7FFFFFFF, 0x00020000);
+        const int vo = (int)(s14_j<LIN>(t, 0) * 8u);   // thread part in the VGPR offset, register part in soffset
 #pragma unroll
         for (int k = 0; k < 16; ++k)
-            raw[k] = __builtin_bit_cast(uint64_t, __builtin_amdgcn_raw_buffer_load_b64(rs, (int)(((k << 10) | t) * 8u), 0, 0));
+            raw[k] = __builtin_bit_cast(uint64_t, __builtin_amdgcn_raw_buffer_load_b64(
+                                                      rs, vo, (int)(s14_j<LIN>(0, (uint32_t)k) * 8u), 0));
     };
     int mod = 0, tmod = -1;
     uint64_t* base = poly(lt, &mod);
@@ -269,36 +279,43 @@ __global__ __launch_bounds__(S14::NT, 1) void ntt14_kernel(PassArgs<TwSrcF> a) {
 #if MFHE_S14_EXP == 2 || MFHE_S14_EXP == 3   // timing probes only (wrong results): 2 = no butterflies, 3 = no butterflies, no exchanges
         if (true) {
 #if MFHE_S14_EXP == 2
-            s14_exchange<0, 1>(x, lds, t);
-            s14_exchange<1, 2>(x, lds, t);
-            s14_exchange<2, 3>(x, lds, t);
-            s14_exchange<3, 0>(x, lds, t);
+            if constexpr (!INV) {
+                s14_exchange<0, 1, true>(x, lds, t);
+                s14_exchange<1, 2, false>(x, lds, t);
+                s14_exchange<2, 3, false>(x, lds, t);
+                s14_exchange<3, 1, false>(x, lds, t);
+            } else {
+                s14_exchange<1, 3, true>(x, lds, t);
+                s14_exchange<3, 2, false>(x, lds, t);
+                s14_exchange<2, 1, false>(x, lds, t);
+                s14_exchange<1, 0, false>(x, lds, t);
+            }
 #endif
         } else
 #endif
         if constexpr (!INV) {
             s14_ct_round<0, 3, 0>(x, ar, tab, btab, t);
-            s14_exchange<0, 1>(x, lds, t);
+            s14_exchange<0, 1, true>(x, lds, t);
 #pragma unroll
             for (int k = 0; k < 16; ++k) x[k] = ar.round_reduce(x[k]);
             s14_ct_round<1, 3, 0>(x, ar, tab, btab, t);
-            s14_exchange<1, 2>(x, lds, t);
+            s14_exchange<1, 2, false>(x, lds, t);
 #pragma unroll
             for (int k = 0; k < 16; ++k) x[k] = ar.round_reduce(x[k]);
             s14_ct_round<2, 3, 1>(x, ar, tab, btab, t);
-            s14_exchange<2, 3>(x, lds, t);
+            s14_exchange<2, 3, false>(x, lds, t);
 #pragma unroll
             for (int k = 0; k < 16; ++k) x[k] = ar.round_reduce(x[k]);
             s14_ct_round<3, 2, 0>(x, ar, tab, btab, t);
-            s14_exchange<3, 0>(x, lds, t);
+            s14_exchange<3, 1, false>(x, lds, t);   // wave-local: each wave stores its block when it is done
         } else {
-            s14_exchange<0, 3>(x, lds, t);
+            s14_exchange<1, 3, true>(x, lds, t);
             s14_gs_round<3, 0, 2>(x, ar, tab, btab, w1, ninv, t);
-            s14_exchange<3, 2>(x, lds, t);
+            s14_exchange<3, 2, false>(x, lds, t);
             s14_gs_round<2, 1, 3>(x, ar, tab, btab, w1, ninv, t);
-            s14_exchange<2, 1>(x, lds, t);
+            s14_exchange<2, 1, false>(x, lds, t);
             s14_gs_round<1, 0, 3>(x, ar, tab, btab, w1, ninv, t);
-            s14_exchange<1, 0>(x, lds, t);
+            s14_exchange<1, 0, false>(x, lds, t);
             s14_gs_round<0, 0, 3>(x, ar, tab, btab, w1, ninv, t);
         }
 #if MFHE_S14_EXP == 1 || MFHE_S14_EXP == 4   // timing probes only: no stores
@@ -306,11 +323,12 @@ __global__ __launch_bounds__(S14::NT, 1) void ntt14_kernel(PassArgs<TwSrcF> a) {
 #endif
         {
             const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(base, 0, 0x7FFFFFFF, 0x00020000);
+            const int vo = (int)(s14_j<LOUT>(s14_opaque(t), 0) * 8u);
 #pragma unroll
             for (int k = 0; k < 16; ++k)
                 __builtin_amdgcn_raw_buffer_store_b64(
-                    __builtin_bit_cast(__attribute__((ext_vector_type(2))) unsigned, ar.canon(x[k])), rs,
-                    (int)(((k << 10) | t) * 8u), 0, MFHE_NTT_CPOL_OUT);
+                    __builtin_bit_cast(__attribute__((ext_vector_type(2))) unsigned, ar.canon(x[k])), rs, vo,
+                    (int)(s14_j<LOUT>(0, (uint32_t)k) * 8u), MFHE_S14_CPOL_OUT);
         }
         if (!more) break;
         lt = nlt;

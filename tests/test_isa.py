@@ -192,7 +192,7 @@ def test_single_pass_14_has_no_memory_traffic_inside_the_transform(inv):
     and must stay in flight through it, so between the loop's prefetch and its 16 stores there is no vector-memory
     instruction (the twiddles come from LDS) and no scratch anywhere (the LICM-hoisted addresses once spilled 102
     VGPRs).  Barriers are LDS-only: no `__syncthreads()` release fence (vmcnt(0)) between the loads and the stores,
-    and three per polynomial (the wave-local exchanges L1 <-> L2 <-> L3 have none)."""
+    and two per polynomial (the wave-local exchanges L1 <-> L2 <-> L3 have none)."""
     asm = _kernel_asm(r"_ZN4mfhe12ntt14_kernelILb%dEEEvNS_8PassArgsINS_6TwSrcFEEE" % inv)
     lines = [ln.split("//")[0].strip() for ln in asm.split("\n") if ln.strip()]
     ops = collections.Counter(re.findall(r"^\s+((?:global|buffer|flat|scratch)_[a-z0-9_]+)", asm, re.M))
@@ -204,11 +204,11 @@ def test_single_pass_14_has_no_memory_traffic_inside_the_transform(inv):
     assert pf_end < st0
     body = lines[pf_end + 1:st0]
     assert not any(re.match(r"(global|buffer|flat)_", ln) for ln in body), "vector memory inside the transform"
-    # r04: only the two cross-wave exchanges (L0 <-> L1 / L3) synchronise the workgroup -- one barrier before the L0
-    # image is written, one after it, one after the last wave-local image -- the wave-local ones wait for their
-    # own LDS writes only (lgkmcnt)
+    # r04: only the cross-wave exchange (L0 <-> L1) synchronises the workgroup -- a barrier before the polynomial's
+    # first LDS image is written and one after the L0 image is written (forward) / before it is read (inverse); the
+    # wave-local exchanges wait for their own LDS writes only (lgkmcnt)
     bars = [i for i, ln in enumerate(body) if ln.startswith("s_barrier")]
-    assert len(bars) == 3, bars
+    assert len(bars) == 2, bars
     # a vmcnt wait inside the transform waits for the prefetch: allowed only after the last barrier (the compiler's
     # loop-carried register copies of the prefetched words), never inside the butterflies
     waits = [i for i, ln in enumerate(body) if "vmcnt" in ln]
