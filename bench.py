@@ -125,6 +125,21 @@ def prof_trace(N, L, batch):
     return best
 
 
+def _warm(fn, min_s=0.05, max_calls=2000):
+    """Untimed calls of fn for at least min_s of wall time (synchronised): the clock ramps over the first ~30 ms of
+    work (profiles/r02_bench_steps.txt).  Single-rank lines only -- a rank-dependent call count would desynchronise
+    the collectives of a multi-rank line."""
+    import torch
+    t_end = time.perf_counter() + min_s
+    for n in range(1, max_calls + 1):
+        fn()
+        if n % 4 == 0:
+            torch.cuda.synchronize()
+            if time.perf_counter() >= t_end:
+                break
+    torch.cuda.synchronize()
+
+
 def other_configs_line(reps=10):
     """The other BASELINE.json NTT shapes on this one GPU (parity cases, not the headline): C2 whole, and the
     per-GPU residue shard of C4 (4 GPUs) and C5 (8 GPUs).  Forward and inverse NTT/s, HIP events.
@@ -213,8 +228,7 @@ def pipeline_line(reps=10):
         ctx.encode(mt, re_, im_)
         ctx.encrypt_pair(re_, im_, sk, cre, cim)
         ctx.decrypt_and_decode(cre, cim, sk, res)
-    run()
-    torch.cuda.synchronize()
+    _warm(run)
     e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
     e0.record()
     for _ in range(reps):
@@ -253,7 +267,7 @@ def trace_line(reps=10):
         ctx.trace_map_bprime(planes[2], planes[3], bp[0], bp[1], n, L, batch)
         gemm()
         ctx.trace_rescale(c[0], c[1], n, L, batch, inv)
-    full()
+    _warm(full)
     torch.cuda.synchronize()
     e = [torch.cuda.Event(enable_timing=True) for _ in range(9)]
     e[0].record()
@@ -336,7 +350,8 @@ def c4_line(world, rank, comm, barrier, reps=5):
             ctx.encode(mt, re_, im_)
             ctx.encrypt_pair(re_, im_, sk, cre, cim)
             ctx.decrypt_and_decode_sharded(c_all, comm, mode, cre, cim, sk, res)
-        run()
+        for _ in range(5):   # a fixed count on every rank (collectives inside)
+            run()
         barrier()
         # HIP events on the stream every call of run() is ordered on (the RCCL exchange included), plus the
         # host wall clock around the same loop; max over ranks of both
