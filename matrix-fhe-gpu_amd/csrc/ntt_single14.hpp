@@ -44,7 +44,7 @@ namespace mfhe {
 struct S14 {
     static constexpr int LOGN = 14, N = 1 << 14, NT = 1024, R = 16;
     static constexpr int TAB = 2048;   // direct twiddles per limb in LDS (stages 0..10)
-    static constexpr size_t LDS_BYTES = (size_t)N * 8 + (size_t)(TAB + 8) * 8;
+    static constexpr size_t LDS_BYTES = (size_t)N * 8 + (size_t)(TAB + 8) * 8 + 16;   // + the drain counter
 };
 
 // LDS slot of element j.  h XORs b5, b6, b7, b8 into bits 0, 2, 3, {1, 4}: every exchange access (ds_write_b64:
@@ -118,9 +118,30 @@ __device__ __forceinline__ void s14_read(double (&x)[16], double* lds, uint32_t 
 // first exchange of a polynomial -- its writes land in blocks another wave may still be reading (the previous
 // polynomial's last exchange); inside a polynomial only the wave itself touches its block between the cross-wave
 // exchanges.
+// Drain counter (r04): instead of a workgroup barrier before a polynomial's first LDS write, each wave adds 1 to an
+// LDS counter after its last read of the previous polynomial's image (a wave's LDS operations are performed in order,
+// so the add lands after those reads), and the first write waits until all 16 waves have added.  A barrier would also
+// wait for everything the other waves issued after their reads -- the output stores (inverse) or a whole round of
+// butterflies (forward).
+// Both in inline asm: the compiler's lowering of an LDS atomic or a volatile LDS load also waits for vmcnt(0), i.e.
+// for the next polynomial's loads in flight.
+__device__ __forceinline__ void s14_drained(uint32_t* cnt) {
+    const uint32_t a = (uint32_t)(size_t)(__attribute__((address_space(3))) uint32_t*)cnt;
+    if ((threadIdx.x & 63) == 0) asm volatile("ds_add_u32 %0, %1" ::"v"(a), "v"(1u) : "memory");   // after this wave's reads
+}
+__device__ __forceinline__ void s14_wait_drained(const uint32_t* cnt, uint32_t target) {
+    const uint32_t a = (uint32_t)(size_t)(const __attribute__((address_space(3))) uint32_t*)cnt;
+    while (true) {
+        uint32_t v;
+        asm volatile("ds_read_b32 %0, %1\n\ts_waitcnt lgkmcnt(0)" : "=v"(v) : "v"(a) : "memory");
+        if (__builtin_amdgcn_readfirstlane(v) >= target) break;
+        __builtin_amdgcn_s_sleep(1);
+    }
+}
 template <int FROM, int TO, bool BAR>
-__device__ __forceinline__ void s14_exchange(double (&x)[16], double* lds, uint32_t t) {
-    if constexpr (BAR) lds_barrier();   // the previous readers of the buffer are done
+__device__ __forceinline__ void s14_exchange(double (&x)[16], double* lds, uint32_t t, const uint32_t* cnt = nullptr,
+                                             uint32_t target = 0) {
+    if constexpr (BAR) s14_wait_drained(cnt, target);   // every wave is done reading the buffer's previous image
     s14_write<FROM>(x, lds, t);
     if constexpr (FROM == 0 || TO == 0) lds_barrier();
     else asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
@@ -204,6 +225,7 @@ __global__ __launch_bounds__(S14::NT, 1) void ntt14_kernel(PassArgs<TwSrcF> a) {
     double* lds = (double*)lds_raw;
     double* tab = lds + S14::N;          // [2048]: tw[0, 2048) of the limb (inverse: itw, entry 1 without n^-1)
     double* btab = tab + S14::TAB;       // [8]: tw[2048 i]
+    uint32_t* drain = (uint32_t*)(btab + 8);   // waves done with the current polynomial's LDS image (s14_drained)
     const uint32_t t = threadIdx.x;
     const uint32_t nb = a.nblocks;       // polynomials (batch * nl)
     uint32_t lt = blockIdx.x;
@@ -231,6 +253,8 @@ __global__ __launch_bounds__(S14::NT, 1) void ntt14_kernel(PassArgs<TwSrcF> a) {
                                                       rs, vo, (int)(s14_j<LIN>(0, (uint32_t)k) * 8u), 0));
     };
     int mod = 0, tmod = -1;
+    uint32_t done = 0;   // polynomials this workgroup has finished: the drain counter's target is 16 done
+    if (t == 0) *drain = 0u;   // published by the first limb's table barriers below
     uint64_t* base = poly(lt, &mod);
     uint64_t raw[16];
     load(base, raw);
@@ -280,22 +304,23 @@ __global__ __launch_bounds__(S14::NT, 1) void ntt14_kernel(PassArgs<TwSrcF> a) {
         if (true) {
 #if MFHE_S14_EXP == 2
             if constexpr (!INV) {
-                s14_exchange<0, 1, true>(x, lds, t);
+                s14_exchange<0, 1, true>(x, lds, t, drain, 16u * done);
                 s14_exchange<1, 2, false>(x, lds, t);
                 s14_exchange<2, 3, false>(x, lds, t);
                 s14_exchange<3, 1, false>(x, lds, t);
             } else {
-                s14_exchange<1, 3, true>(x, lds, t);
+                s14_exchange<1, 3, true>(x, lds, t, drain, 16u * done);
                 s14_exchange<3, 2, false>(x, lds, t);
                 s14_exchange<2, 1, false>(x, lds, t);
                 s14_exchange<1, 0, false>(x, lds, t);
             }
+            s14_drained(drain);
 #endif
         } else
 #endif
         if constexpr (!INV) {
             s14_ct_round<0, 3, 0>(x, ar, tab, btab, t);
-            s14_exchange<0, 1, true>(x, lds, t);
+            s14_exchange<0, 1, true>(x, lds, t, drain, 16u * done);
 #pragma unroll
             for (int k = 0; k < 16; ++k) x[k] = ar.round_reduce(x[k]);
             s14_ct_round<1, 3, 0>(x, ar, tab, btab, t);
@@ -308,16 +333,19 @@ __global__ __launch_bounds__(S14::NT, 1) void ntt14_kernel(PassArgs<TwSrcF> a) {
             for (int k = 0; k < 16; ++k) x[k] = ar.round_reduce(x[k]);
             s14_ct_round<3, 2, 0>(x, ar, tab, btab, t);
             s14_exchange<3, 1, false>(x, lds, t);   // wave-local: each wave stores its block when it is done
+            s14_drained(drain);
         } else {
-            s14_exchange<1, 3, true>(x, lds, t);
+            s14_exchange<1, 3, true>(x, lds, t, drain, 16u * done);
             s14_gs_round<3, 0, 2>(x, ar, tab, btab, w1, ninv, t);
             s14_exchange<3, 2, false>(x, lds, t);
             s14_gs_round<2, 1, 3>(x, ar, tab, btab, w1, ninv, t);
             s14_exchange<2, 1, false>(x, lds, t);
             s14_gs_round<1, 0, 3>(x, ar, tab, btab, w1, ninv, t);
             s14_exchange<1, 0, false>(x, lds, t);
+            s14_drained(drain);
             s14_gs_round<0, 0, 3>(x, ar, tab, btab, w1, ninv, t);
         }
+        ++done;
 #if MFHE_S14_EXP == 1 || MFHE_S14_EXP == 4   // timing probes only: no stores
         if (lt == 0xFFFFFFFFu)
 #endif

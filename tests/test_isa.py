@@ -192,7 +192,7 @@ def test_single_pass_14_has_no_memory_traffic_inside_the_transform(inv):
     and must stay in flight through it, so between the loop's prefetch and its 16 stores there is no vector-memory
     instruction (the twiddles come from LDS) and no scratch anywhere (the LICM-hoisted addresses once spilled 102
     VGPRs).  Barriers are LDS-only: no `__syncthreads()` release fence (vmcnt(0)) between the loads and the stores,
-    and two per polynomial (the wave-local exchanges L1 <-> L2 <-> L3 have none)."""
+    and one per polynomial (the wave-local exchanges L1 <-> L2 <-> L3 have none, the first write waits on a counter)."""
     asm = _kernel_asm(r"_ZN4mfhe12ntt14_kernelILb%dEEEvNS_8PassArgsINS_6TwSrcFEEE" % inv)
     lines = [ln.split("//")[0].strip() for ln in asm.split("\n") if ln.strip()]
     ops = collections.Counter(re.findall(r"^\s+((?:global|buffer|flat|scratch)_[a-z0-9_]+)", asm, re.M))
@@ -200,16 +200,17 @@ def test_single_pass_14_has_no_memory_traffic_inside_the_transform(inv):
     assert ops["buffer_load_dwordx2"] == 32 and ops["buffer_store_dwordx2"] == 16, ops
     loads = [i for i, ln in enumerate(lines) if ln.startswith("buffer_load_dwordx2")]
     stores = [i for i, ln in enumerate(lines) if ln.startswith("buffer_store_dwordx2")]
-    pf_end, st0 = loads[-1], stores[0]   # the in-loop prefetch is the second group of 16 loads
-    assert pf_end < st0
-    body = lines[pf_end + 1:st0]
-    assert not any(re.match(r"(global|buffer|flat)_", ln) for ln in body), "vector memory inside the transform"
-    # r04: only the cross-wave exchange (L0 <-> L1) synchronises the workgroup -- a barrier before the polynomial's
-    # first LDS image is written and one after the L0 image is written (forward) / before it is read (inverse); the
-    # wave-local exchanges wait for their own LDS writes only (lgkmcnt)
+    pf_end = loads[-1]   # the in-loop prefetch is the second group of 16 loads
+    # the transform runs from the prefetch to the first store in execution order: straight down when the stores
+    # follow the prefetch in the code, else down to the loop's back-edge (a rotated loop keeps its stores first)
+    body = lines[pf_end + 1:stores[0]] if stores[0] > pf_end else lines[pf_end + 1:]
+    assert not any(re.match(r"(global|buffer|flat|scratch)_", ln) for ln in body), "vector memory inside the transform"
+    # r04: one workgroup barrier per polynomial, after the cross-wave L0 image is written; the polynomial's first LDS
+    # write waits on an LDS drain counter (ds_add_u32 / ds_read_b32 in inline asm), the wave-local exchanges wait for
+    # their own LDS writes only (lgkmcnt)
     bars = [i for i, ln in enumerate(body) if ln.startswith("s_barrier")]
-    assert len(bars) == 2, bars
-    # a vmcnt wait inside the transform waits for the prefetch: allowed only after the last barrier (the compiler's
-    # loop-carried register copies of the prefetched words), never inside the butterflies
-    waits = [i for i, ln in enumerate(body) if "vmcnt" in ln]
-    assert not waits or min(waits) > bars[-1], (waits[:3], bars)
+    assert len(bars) == 1, bars
+    assert sum(ln.startswith("ds_add_u32") for ln in body) == 1
+    # no vmcnt wait inside the transform: it would wait for the prefetch
+    waits = [ln for ln in body if "vmcnt" in ln]
+    assert not waits, waits[:3]
