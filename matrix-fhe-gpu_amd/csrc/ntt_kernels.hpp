@@ -53,7 +53,12 @@ struct TwSrcF {
 struct TwSrcU {
     const uint64_t* w;
     const uint64_t* ws;
-    __device__ __forceinline__ ulonglong2 get(size_t i) const { return make_ulonglong2(w[i], ws[i]); }
+    __device__ __forceinline__ ulonglong2 get(size_t i) const {
+#ifdef MFHE_EXP_TWCONST   // timing probe only (wrong results): twiddles computed from the index, no loads
+        return make_ulonglong2((uint64_t)i * 0x9E3779B97F4A7C15ull >> 6, (uint64_t)i * 0xC2B2AE3D27D4EB4Full);
+#endif
+        return make_ulonglong2(w[i], ws[i]);
+    }
 };
 
 template <class TS>

@@ -68,6 +68,9 @@ struct NttJob {
     mfhe_ctx* ctx;        // owning context (null: raw phantom entry)
 };
 
+#ifndef MFHE_NTT_U64_BLOCK_PF
+#define MFHE_NTT_U64_BLOCK_PF 0   // A/B: the U64 block passes with the next tile's loads issued before the butterflies
+#endif
 template <class A, class TS, int LOG_G, int LOG_R, int NG, bool COLS, bool INV, bool IN_RAW, bool OUT_RAW, bool TWIST,
           bool BREV, bool UNI, bool PACK = false>
 static int launch_pass(const NttJob<TS>& j, int s0, hipStream_t st) {
@@ -98,11 +101,12 @@ static int launch_pass(const NttJob<TS>& j, int s0, hipStream_t st) {
     a.nblocks = (uint32_t)nb;
     const bool need_lds = (Gm::NR > 1) || BREV;
     const size_t lds = need_lds ? (size_t)NG * Gm::GS * sizeof(uint64_t) : 0;
-    auto kern = j.prefetch == 1 ? ntt_pass_kernel<A, TS, LOG_G, LOG_R, NG, COLS, INV, IN_RAW, OUT_RAW, TWIST, BREV, UNI, true, PACK>
-                           : ntt_pass_kernel<A, TS, LOG_G, LOG_R, NG, COLS, INV, IN_RAW, OUT_RAW, TWIST, BREV, UNI, false, PACK>;
+    const bool pf = j.prefetch == 1 || (MFHE_NTT_U64_BLOCK_PF && std::is_same<A, ArithU64>::value && !COLS);
+    auto kern = pf ? ntt_pass_kernel<A, TS, LOG_G, LOG_R, NG, COLS, INV, IN_RAW, OUT_RAW, TWIST, BREV, UNI, true, PACK>
+                   : ntt_pass_kernel<A, TS, LOG_G, LOG_R, NG, COLS, INV, IN_RAW, OUT_RAW, TWIST, BREV, UNI, false, PACK>;
     // persistent grid: resident workgroups only (occupancy query cached per instantiation), a multiple of 8
     static int occ_cache[2] = {0, 0};
-    int& occ = occ_cache[j.prefetch == 1 ? 1 : 0];
+    int& occ = occ_cache[pf ? 1 : 0];
     if (occ == 0) {
         int o = 0;
         if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&o, kern, NT, lds) != hipSuccess || o < 1) o = 1;
