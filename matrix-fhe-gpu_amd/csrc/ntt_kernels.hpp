@@ -40,6 +40,9 @@
 #ifndef MFHE_NTT_CPOL_MID_ST
 #define MFHE_NTT_CPOL_MID_ST 0
 #endif
+#ifndef MFHE_NTT_U64_INV_TWPRE
+#define MFHE_NTT_U64_INV_TWPRE 1   // +4% U64 inverse (profiles/r04_u64_block_variants.txt)
+#endif
 #ifndef MFHE_NTT_COL_DMA
 #define MFHE_NTT_COL_DMA 1   // forward column pass: tile -> LDS by LDS-DMA (16 B per lane), no VGPR staging
 #endif
@@ -348,6 +351,18 @@ struct NttPass {
             for (int k = 0; k < R; ++k) x[k] = A::from_raw(my_lds[Gm::pad(Gm::g_of(r_to, tau_, k))]);
         };
 
+        // U64 inverse block pass (MFHE_NTT_U64_INV_TWPRE, default on): the first executed stage's (w, w') pairs are loaded
+        // before the entry exchange, so their latency overlaps it instead of following it (profiles/
+        // r04_u64_twiddle_probe.txt: the inverse's first pass waits on these loads, the forward's passes do not)
+        constexpr bool kTwPre = INV && !COLS && std::is_same<A, ArithU64>::value && MFHE_NTT_U64_INV_TWPRE;
+        Tw wpre[kTwPre ? R / 2 : 1];
+        if constexpr (kTwPre) {
+            constexpr int r = NR - 1, wl = Gm::WL(r), bit = wl;   // bb = 0
+            const int s = s0 + (LOG_G - 1 - bit);
+            const uint64_t twb = twoff + (1ull << s) + (L.hi << (LOG_G - 1 - bit)) + ((uint64_t)(tau_ >> wl) << (LOG_R - 1));
+#pragma unroll
+            for (int m = 0; m < R / 2; ++m) wpre[m] = a.tw.get(twb + (uint64_t)m);
+        }
         if constexpr (INV && !COLS && (NR > 1 || BREV))
             exchange(std::integral_constant<int, 0>{}, std::integral_constant<int, NR - 1>{}, BREV);
 
@@ -390,7 +405,9 @@ struct NttPass {
 #pragma unroll
                         for (int k = 0; k < R; ++k) {
                             if (k & half) continue;
-                            const Tw w = a.tw.get(twb + (uint64_t)(k >> (bb + 1)));
+                            Tw w;
+                            if constexpr (kTwPre && r == NR - 1 && bb == 0) w = wpre[k >> 1];
+                            else w = a.tw.get(twb + (uint64_t)(k >> (bb + 1)));
                             if constexpr (e % 2 == 0) ar.gs_lazy(x[k], x[k + half], w);
                             else ar.gs(x[k], x[k + half], w);
                         }
@@ -529,9 +546,19 @@ constexpr int min_waves_per_simd(int nt) {
     return (MFHE_NTT_MIN_WG_CU * nt / 256) < 1 ? 1 : (MFHE_NTT_MIN_WG_CU * nt / 256);
 }
 
+// U64 block passes (A/B, MFHE_NTT_U64_BLOCK_W4): registers held to 4 waves per SIMD (128 VGPRs); the inverse's first
+// pass otherwise compiles to 129 and runs 3
+#ifndef MFHE_NTT_U64_BLOCK_W4
+#define MFHE_NTT_U64_BLOCK_W4 0
+#endif
+template <class A, bool COLS>
+constexpr int pass_min_waves(int nt) {
+    return (MFHE_NTT_U64_BLOCK_W4 && std::is_same<A, ArithU64>::value && !COLS && nt <= 256) ? 4 : min_waves_per_simd(nt);
+}
+
 template <class A, class TS, int LOG_G, int LOG_R, int NG, bool COLS, bool INV, bool IN_RAW, bool OUT_RAW,
           bool TWIST, bool BREV, bool UNI, bool PF, bool PACK = false>
-__global__ __launch_bounds__(NG * (1 << (LOG_G - LOG_R)), min_waves_per_simd(NG * (1 << (LOG_G - LOG_R))))
+__global__ __launch_bounds__(NG * (1 << (LOG_G - LOG_R)), (pass_min_waves<A, COLS>(NG * (1 << (LOG_G - LOG_R)))))
 void ntt_pass_kernel(PassArgs<TS> a) {
     extern __shared__ __attribute__((aligned(16))) uint64_t lds[];
     pass_loop<NttPass<A, TS, LOG_G, LOG_R, NG, COLS, INV, IN_RAW, OUT_RAW, TWIST, BREV, UNI, PACK>, PF>(a, lds);
