@@ -34,6 +34,9 @@
 #ifndef MFHE_S14_CPOL_OUT
 #define MFHE_S14_CPOL_OUT MFHE_NTT_CPOL_OUT   // output store policy (gfx950 CPol bits: 1 sc0, 2 nt, 16 sc1)
 #endif
+#ifndef MFHE_S14_LATE_CVT
+#define MFHE_S14_LATE_CVT 1   // +1-2% (profiles/r04_c2_late_cvt_ab.txt)
+#endif
 #ifndef MFHE_S14_EXP
 #define MFHE_S14_EXP 0   // timing probes (wrong results), never in the product build: 1 compute only, 2 exchanges +
                          // memory, 3 memory only, 4 no stores, 5 no loads after the first
@@ -258,6 +261,14 @@ __global__ __launch_bounds__(S14::NT, 1) void ntt14_kernel(PassArgs<TwSrcF> a) {
     uint64_t* base = poly(lt, &mod);
     uint64_t raw[16];
     load(base, raw);
+    // the polynomial's words are converted at the END of the previous iteration, after its stores: the loop then
+    // carries the converted doubles, so the compiler's loop-carried register copies no longer wait (vmcnt) for the
+    // prefetch in the middle of the store sequence (r04, MFHE_S14_LATE_CVT)
+    double x[16];
+    if constexpr (MFHE_S14_LATE_CVT) {
+#pragma unroll
+        for (int k = 0; k < 16; ++k) x[k] = ArithF64::from_u64(raw[k]);
+    }
     ArithF64 ar(LimbConst{});
     double w1 = 0.0, ninv = 0.0;
     while (true) {
@@ -289,9 +300,10 @@ __global__ __launch_bounds__(S14::NT, 1) void ntt14_kernel(PassArgs<TwSrcF> a) {
             }
             lds_barrier();
         }
-        double x[16];
+        if constexpr (!MFHE_S14_LATE_CVT) {
 #pragma unroll
-        for (int k = 0; k < 16; ++k) x[k] = ArithF64::from_u64(raw[k]);
+            for (int k = 0; k < 16; ++k) x[k] = ArithF64::from_u64(raw[k]);
+        }
         uint64_t* nbase = base;
         int nmod = mod;
         if (more) {
@@ -359,6 +371,10 @@ __global__ __launch_bounds__(S14::NT, 1) void ntt14_kernel(PassArgs<TwSrcF> a) {
                     (int)(s14_j<LOUT>(0, (uint32_t)k) * 8u), MFHE_S14_CPOL_OUT);
         }
         if (!more) break;
+        if constexpr (MFHE_S14_LATE_CVT) {
+#pragma unroll
+            for (int k = 0; k < 16; ++k) x[k] = ArithF64::from_u64(raw[k]);
+        }
         lt = nlt;
         base = nbase;
         mod = nmod;
