@@ -1,6 +1,7 @@
 // gemm.hip -- see gemm.hpp.
 #include "gemm.hpp"
 #include "mfhe_ctx.hpp"
+#include "ring_row.hpp"
 
 namespace mfhe {
 
@@ -747,6 +748,146 @@ __global__ __launch_bounds__(256) void mfma_digitize_ifold_kernel(ModGemmArgs a,
     }
 }
 
+// The same digitize with the decrypt fused in front of it (n = 64, he.hip mfhe_decrypt_and_decode): B is never
+// written to HBM.  One workgroup owns limb l and row y: the 64 columns p = 64 y + x over all 512 k (= w), so the
+// whole X row of every (w, l, y) -- what the ring product needs -- is inside the workgroup, and the column sums
+// s0 / s1 / s2 stay in it.  Per 32-k panel kc (eight iterations):
+//   ring: 64 rows w = a' 256 + 32 kc + (0..31) (a' = 0, 1), 16 lanes per row (ring_row.hpp), B = ct.b +
+//         INTT(NTT(ct.a) s) mod q exactly as dec_ring_kernel, reduced as the digitize reduces it, into LDS [row][x];
+//   digitize: wave c = 2 a' + hf takes the 16 k of (a', hf) at column x = lane, the four waves fill each column's
+//         64-byte (a', hf) group of the kc plane: 4 KiB contiguous per plane and iteration.
+// Reads: ct (16 B per element) + s (L2-resident); writes: the digit planes.  The B round trip of the unfused path
+// (8 B written by dec_ring_kernel + 8 B read here per element) and one launch per component are gone.
+template <int D>
+__global__ __launch_bounds__(256) void mfma_digitize_ifold_dec_kernel(ModGemmArgs a, uint32_t Ppad, PlaneCounts pc) {
+    constexpr int LOGN = 6, N = 64, RS = N + 2;   // row stride 528 B: the ring's 16-B row writes spread over banks
+    __shared__ __attribute__((aligned(16))) double bt[64 * RS];
+    const int t = threadIdx.x, lane = t & 63, wv = t >> 6;
+    const uint32_t y = blockIdx.x;
+    const int l = blockIdx.y, L = gridDim.y;
+    typedef const __attribute__((address_space(4))) double* cdp_t;
+    const cdp_t fo = (cdp_t)(a.ifold + (uint64_t)l * 16);
+    LimbConst lc;
+    lc.qf = fo[0];
+    lc.qinv = fo[1];
+    const ArithF64 ar(lc);
+    const LimbConst rl = ((const LimbConst*)a.dlf)[l];
+    const ArithF64 rar(rl);
+    const double* izl = a.iz + (uint64_t)l * 48;
+    const double x1 = ((cdp_t)izl)[0], x2 = ((cdp_t)izl)[1];
+    const double* zp = izl + 16;
+    const int nd = l < 64 ? pc.n[l] : D;
+    // ring-stage lane: 4 coefficients 4 j .. 4 j + 3 of row 16 s + rs (s = 0..3)
+    const int j = t & 15, rs = t >> 4;
+    const double* tw = a.dtw + (uint64_t)l * N;
+    const double* itw = a.ditw + (uint64_t)l * N;
+    const double ninv = a.dninv[l];
+    // digitize-stage lane: column x = lane, (a', hf) = wave
+    const int ap = wv >> 1, hf = wv & 1;
+    const uint32_t p = y * N + lane;
+    double s0 = 0.0, s1 = 0.0, s2 = 0.0;
+    // all four substeps' loads are issued before the first ring product (measured: a one-substep-ahead rolling
+    // prefetch needs 186 VGPRs, 2 workgroups per CU, or spills at 3: 2-5% slower, profiles/r04_dec_fused_ab.txt)
+#pragma unroll 1
+    for (int kc = 0; kc < FK / 32; ++kc) {
+        uint64_t av[4][4], sk[4][4], bv[4][4];
+#pragma unroll
+        for (int st = 0; st < 4; ++st) {
+            const int rr = st * 16 + rs;
+            const uint64_t w = (uint64_t)(rr >> 5) * FK + kc * 32 + (rr & 31);
+            const uint64_t wl = w * L + l, r0 = (wl * N + y) * N;
+            ld4(a.dct + a.dtotal + r0 + 4 * j, av[st]);
+            ld4(a.dsk + wl * N + 4 * j, sk[st]);
+            ld4(a.dct + r0 + 4 * j, bv[st]);
+        }
+        // ring product per row (the shuffle ring_mul_row: ring_mul_row64_lds measured slower here, 198 vs 183 us)
+#pragma unroll
+        for (int st = 0; st < 4; ++st) {
+            double x[4], sv[4];
+#pragma unroll
+            for (int e = 0; e < 4; ++e) {
+                x[e] = ArithF64::from_u64(av[st][e]);
+                sv[e] = centred_f(sk[st][e], rl.qf);
+            }
+            ring_mul_row<LOGN>(x, sv, j, rar, tw, itw, ninv);
+            double v[4];
+#pragma unroll
+            for (int e = 0; e < 4; ++e) {
+                const uint64_t sum = bv[st][e] + rar.canon(x[e]);
+                v[e] = ar.reduce(ArithF64::from_u64(sum >= rl.q ? sum - rl.q : sum));
+            }
+            double* row = bt + (st * 16 + rs) * RS + 4 * j;
+            *(double2*)row = make_double2(v[0], v[1]);
+            *(double2*)(row + 2) = make_double2(v[2], v[3]);
+        }
+        __syncthreads();
+        const int k0 = kc * 32 + hf * 16;
+        double v[16];
+#pragma unroll
+        for (int kk = 0; kk < 16; ++kk) v[kk] = bt[(wv * 16 + kk) * RS + lane];   // b = k0 + kk + 1 of a = a' + 1
+        // as mfma_digitize_ifold_kernel: Horner chains for x1, x2 and the plain sum over this chunk
+        double h1 = v[15], h2 = v[15], t0 = 0.0;
+#pragma unroll
+        for (int kk = 14; kk >= 0; --kk) {
+            h1 = ar.mulmod(h1, x1) + v[kk];
+            h2 = ar.mulmod(h2, x2) + v[kk];
+        }
+#pragma unroll
+        for (int kk = 0; kk < 16; ++kk) t0 += v[kk];
+        s0 = ar.reduce(s0 + t0);
+        s1 = ar.reduce(s1 + ar.mulmod(h1, zp[(k0 >> 4)]));
+        s2 = ar.reduce(s2 + ar.mulmod(h2, zp[16 + (k0 >> 4)]));
+        uint32_t pk[D][4];
+#pragma unroll
+        for (int i = 0; i < D; ++i)
+#pragma unroll
+            for (int c = 0; c < 4; ++c) pk[i][c] = 0;
+#pragma unroll
+        for (int kk = 0; kk < 16; ++kk) {
+            const uint64_t yb = balanced_bytes<D>(v[kk]);
+            const uint32_t lo = (uint32_t)yb, hi = (uint32_t)(yb >> 32);
+#pragma unroll
+            for (int i = 0; i < D; ++i) {
+                const uint32_t b = i < 4 ? (lo >> (8 * i)) & 255u : (hi >> (8 * (i - 4))) & 255u;
+                pk[i][kk >> 2] |= b << (8 * (kk & 3));
+            }
+        }
+#pragma unroll
+        for (int i = 0; i < D; ++i) {
+            if (i >= nd) break;
+            int8_t* o = a.Bdig + (((uint64_t)l * D + i) * (FK / 32) + kc) * (uint64_t)Ppad * 64 + (uint64_t)p * 64 + wv * 16;
+            const uint32_t* w = pk[i];
+            *(v4i*)o = v4i{(int)(w[0] ^ 0x80808080u), (int)(w[1] ^ 0x80808080u), (int)(w[2] ^ 0x80808080u),
+                           (int)(w[3] ^ 0x80808080u)};
+        }
+        __syncthreads();   // the next panel's ring stage rewrites bt
+    }
+    // column sums: (a', hf) are the four waves
+    bt[(0 * 4 + wv) * 64 + lane] = s0;
+    bt[(1 * 4 + wv) * 64 + lane] = s1;
+    bt[(2 * 4 + wv) * 64 + lane] = s2;
+    __syncthreads();
+    if (wv != 0) return;
+    double e1[3], e2[3];   // a = 1 (a' = 0), a = 2 (a' = 1)
+#pragma unroll
+    for (int tt = 0; tt < 3; ++tt) {
+        e1[tt] = ar.reduce(bt[(tt * 4 + 0) * 64 + lane] + bt[(tt * 4 + 1) * 64 + lane]);
+        e2[tt] = ar.reduce(bt[(tt * 4 + 2) * 64 + lane] + bt[(tt * 4 + 3) * 64 + lane]);
+    }
+    const double h0 = ar.mulmod(e1[0], fo[2]) + ar.mulmod(e2[0], fo[5]);
+    const double h257 = ar.mulmod(e1[0], fo[8]) + ar.mulmod(e2[0], fo[11]);
+    const double h512 = ar.mulmod(e1[1], fo[8]) + ar.mulmod(e2[1], fo[11]);
+    const double h513 = ar.mulmod(e1[2], fo[9]) + ar.mulmod(e2[2], fo[12]);
+    auto phi = [&](int byte, int sh) { return (double)((int)((a.phi[byte] >> sh) & 3) - 1); };
+    const double c1 = ar.reduce(h513);
+    const double c0 = ar.reduce(h512 - c1 * phi(254, 6));
+    uint64_t* Cl = a.C + (uint64_t)l * a.cL + (uint64_t)y * a.scY + lane;
+    Cl[0] = ar.canon(h0 - c0 * phi(256, 0));
+    Cl[257 * a.scM] = ar.canon(h257 - c0 * phi(256, 4) - c1 * phi(256, 6));
+    a.cc[((uint64_t)l * Ppad + p) * 2] = c0;
+    a.cc[((uint64_t)l * Ppad + p) * 2 + 1] = c1;
+}
+
 // C = sum_s acc_s * 256^s mod q for the 32 x 32 wave tile at (m0, p0) of limb l (lane = (r, h)).
 // MODE 1 (factored forward): column p0 + r is (a', p) = divmod(., Ppad), output row a' * 256 + row, plus d0.
 // MODE 2 (factored inverse): column p0 + r is 2 p + a', row r2 - 1; lanes r, r ^ 1 hold a' = 0, 1 of one column
@@ -1272,11 +1413,21 @@ static int launch_factored_inv(const ModGemmArgs& a, int L, hipStream_t s) {
     const uint32_t Ppad = (a.P + 63) / 64 * 64;
     ModGemmArgs f = a;
     f.cc = (double*)(a.Bdig + (size_t)L * a.D * Ppad * MK);   // the d0 region: L * Ppad * 2 doubles
-    const dim3 gd(Ppad / 16, L);
     const PlaneCounts pc = plane_counts(a, L);
-    if (a.D == 5) hipLaunchKernelGGL(mfma_digitize_ifold_kernel<5>, gd, dim3(256), 0, s, f, Ppad, pc);
-    else hipLaunchKernelGGL(mfma_digitize_ifold_kernel<6>, gd, dim3(256), 0, s, f, Ppad, pc);
-    MFHE_CHECK_LAUNCH("mfma_digitize_ifold_kernel");
+    if (a.dct) {
+        // decrypt fused (n = 64 rows: one workgroup per (y, l), 64 columns)
+        if (a.log_n != 6 || a.P != 64u * 64u || Ppad != a.P || !a.dsk || !a.dlf || !a.dtw || !a.ditw || !a.dninv)
+            return set_error(MFHE_EINVAL, "mod_gemm: the decrypt-fused inverse W-CRT needs n = 64 and the ring tables");
+        const dim3 gr(64, L);
+        if (a.D == 5) hipLaunchKernelGGL(mfma_digitize_ifold_dec_kernel<5>, gr, dim3(256), 0, s, f, Ppad, pc);
+        else hipLaunchKernelGGL(mfma_digitize_ifold_dec_kernel<6>, gr, dim3(256), 0, s, f, Ppad, pc);
+        MFHE_CHECK_LAUNCH("mfma_digitize_ifold_dec_kernel");
+    } else {
+        const dim3 gd(Ppad / 16, L);
+        if (a.D == 5) hipLaunchKernelGGL(mfma_digitize_ifold_kernel<5>, gd, dim3(256), 0, s, f, Ppad, pc);
+        else hipLaunchKernelGGL(mfma_digitize_ifold_kernel<6>, gd, dim3(256), 0, s, f, Ppad, pc);
+        MFHE_CHECK_LAUNCH("mfma_digitize_ifold_kernel");
+    }
     if (launch_ring56<2>(f, L, Ppad, s)) {
         MFHE_CHECK_LAUNCH("mod_gemm_mfma_ring56_kernel (factored inverse)");
         return MFHE_OK;
@@ -1295,6 +1446,7 @@ static int launch_factored_inv(const ModGemmArgs& a, int L, hipStream_t s) {
 }
 
 int launch_mod_gemm(const ModGemmArgs& a, int L, hipStream_t s) {
+    if (a.dct && !(a.Adig && a.ifold)) return set_error(MFHE_EINVAL, "mod_gemm: a decrypt-fused B needs the factored inverse");
     if (a.Adig && a.ifold) {
         if (a.M != 512 || a.K != MK || !a.epi || a.D < 5 || a.D > 6 || !a.lds_stage || !a.iz || !a.phi)
             return set_error(MFHE_EINVAL, "mod_gemm: factored inverse W-CRT needs M = K = 512, the FP64 epilogue and D in {5, 6}");

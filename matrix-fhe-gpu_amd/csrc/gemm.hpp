@@ -60,6 +60,16 @@ struct ModGemmArgs {
     uint64_t qf_row = 0, qf_step = 0;
     double delta = 0.0;
     int lbase = 0, Ltot = 0;
+    // factored inverse only (n = 64): B is not read; the digitize kernel forms it as the decrypt of the ciphertext
+    // dct (gemm.hip mfma_digitize_ifold_dec_kernel): B[w][l][y][.] = ct.b + INTT(NTT(ct.a) * s) mod q over each
+    // X row (ring_row.hpp, he.hip dec_ring_kernel), ct matrix-major, b at dct and a at dct + dtotal
+    const uint64_t* dct = nullptr;
+    uint64_t dtotal = 0;
+    const uint64_t* dsk = nullptr;    // s [w][L][n], NTT form
+    const void* dlf = nullptr;        // LimbConst [L]
+    const double* dtw = nullptr;      // X-NTT tables [L][n] (ph_f)
+    const double* ditw = nullptr;
+    const double* dninv = nullptr;    // [L]
 };
 
 // bytes of B digit workspace the MFMA path needs for P columns and L limbs at D digits

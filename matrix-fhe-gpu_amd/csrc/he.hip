@@ -15,6 +15,7 @@
 
 #include "gemm.hpp"
 #include "mfhe_ctx.hpp"
+#include "ring_row.hpp"
 
 extern "C" int mfhe_ntt_fwd(mfhe_ctx*, uint64_t*, size_t, int, int, mfhe_stream_t);
 extern "C" int mfhe_ntt_inv(mfhe_ctx*, uint64_t*, size_t, int, int, mfhe_stream_t);
@@ -183,111 +184,6 @@ __global__ __launch_bounds__(256) void enc_combine_kernel(const uint64_t* __rest
     }
 }
 
-// ---------------- fused X-axis ring product (n = 4..64) ----------------
-// t = INTT(NTT(a) (.) s) for one length-n row, phantom convention (the ph tables of mfhe_ntt_fwd/_inv, so
-// s = mfhe_ntt_fwd(secret) is in the matching order): the reference's xy_ntt_forward_phantom ->
-// pointwise_mul_s_kernel -> xy_ntt_backward_phantom (HE.cu:1500-1530, 1575-1590) without the three HBM
-// round trips.  T = n/4 lanes per row, lane j holds coefficients 4j..4j+3; butterflies at distance
-// t >= 4 pair lane j with lane j ^ (t/4), each lane of the pair computing two of the four butterflies;
-// t = 1, 2 stay in the lane.
-// FP64 exact modmul (ntt_arith.hpp); bounds: |mulmod| <= 1.5 q, forward values are re-centred every two
-// stages (|v| <= 2 q into a mulmod), inverse X every stage (|u - v| <= 3 q), q < 2^50.
-template <int LOGN>
-__device__ __forceinline__ void ring_mul_row(double (&x)[4], const double (&sv)[4], int j, const ArithF64& ar,
-                                             const double* __restrict__ tw, const double* __restrict__ itw,
-                                             double ninv) {
-#pragma unroll
-    for (int st = 0; st < LOGN; ++st) {   // forward CT: m = 2^st, t = n / 2m, W = tw[m + k / 2t]
-        const int m = 1 << st, lt = LOGN - 1 - st, t = 1 << lt;
-        if (t >= 4) {
-            // lanes j (lower) and j ^ d (upper) pair slot by slot; the lower lane computes slots 0, 1 and the
-            // upper slots 2, 3 (two shuffles in, two out, two modmuls per lane)
-            const int d = t >> 2;
-            const bool up = j & d;
-#pragma unroll
-            for (int k = 0; k < 2; ++k) {
-                const double recv = __shfl_xor(up ? x[k] : x[k + 2], d);
-                const double u = up ? recv : x[k], v = up ? x[k + 2] : recv;
-                const double mv = ar.mulmod(v, tw[m + ((4 * j + (up ? k + 2 : k)) >> (lt + 1))]);
-                const double X = u + mv, Y = u - mv;
-                const double back = __shfl_xor(up ? X : Y, d);
-                x[k] = up ? back : X;
-                x[k + 2] = up ? Y : back;
-            }
-        } else if (t == 2) {
-            const double w = tw[m + j];
-#pragma unroll
-            for (int a = 0; a < 2; ++a) {
-                const double mv = ar.mulmod(x[a + 2], w);
-                x[a + 2] = x[a] - mv;
-                x[a] += mv;
-            }
-        } else {
-#pragma unroll
-            for (int a = 0; a < 4; a += 2) {
-                const double mv = ar.mulmod(x[a + 1], tw[m + 2 * j + a / 2]);
-                x[a + 1] = x[a] - mv;
-                x[a] += mv;
-            }
-        }
-        if ((st & 1) || st == LOGN - 1)
-#pragma unroll
-            for (int s = 0; s < 4; ++s) x[s] = ar.reduce(x[s]);
-    }
-#pragma unroll
-    for (int s = 0; s < 4; ++s) x[s] = ar.mulmod(x[s], sv[s]);
-#pragma unroll
-    for (int st = LOGN - 1; st >= 0; --st) {   // inverse GS: X = u + v, Y = (u - v) W; m = 1 scales by n^-1
-        const int m = 1 << st, lt = LOGN - 1 - st, t = 1 << lt;
-        const bool last = st == 0;
-        auto xsum = [&](double u) { return last ? ar.mulmod(u, ninv) : ar.reduce(u); };
-        if (t >= 4) {
-            const int d = t >> 2;
-            const bool up = j & d;
-#pragma unroll
-            for (int k = 0; k < 2; ++k) {
-                const double recv = __shfl_xor(up ? x[k] : x[k + 2], d);
-                const double u = up ? recv : x[k], v = up ? x[k + 2] : recv;
-                const double X = xsum(u + v);
-                const double Y = ar.mulmod(u - v, itw[m + ((4 * j + (up ? k + 2 : k)) >> (lt + 1))]);
-                const double back = __shfl_xor(up ? X : Y, d);
-                x[k] = up ? back : X;
-                x[k + 2] = up ? Y : back;
-            }
-        } else if (t == 2) {
-            const double w = itw[m + j];
-#pragma unroll
-            for (int a = 0; a < 2; ++a) {
-                const double u = x[a], v = x[a + 2];
-                x[a] = xsum(u + v);
-                x[a + 2] = ar.mulmod(u - v, w);
-            }
-        } else {
-#pragma unroll
-            for (int a = 0; a < 4; a += 2) {
-                const double u = x[a], v = x[a + 1];
-                x[a] = xsum(u + v);
-                x[a + 1] = ar.mulmod(u - v, itw[m + 2 * j + a / 2]);
-            }
-        }
-    }
-}
-
-// 4 consecutive u64 (32-byte aligned) as two 16-byte accesses
-__device__ __forceinline__ void ld4(const uint64_t* p, uint64_t (&v)[4]) {
-    const ulonglong2 a = *(const ulonglong2*)p, b = *(const ulonglong2*)(p + 2);
-    v[0] = a.x; v[1] = a.y; v[2] = b.x; v[3] = b.y;
-}
-__device__ __forceinline__ void st4(uint64_t* p, const uint64_t (&v)[4]) {
-    *(ulonglong2*)p = make_ulonglong2(v[0], v[1]);
-    *(ulonglong2*)(p + 2) = make_ulonglong2(v[2], v[3]);
-}
-
-__device__ __forceinline__ double centred_f(uint64_t v, double q) {
-    const double d = ArithF64::from_u64(v);
-    return d > 0.5 * q ? d - q : d;
-}
-
 struct RingArgs {
     const LimbConst* lf;     // [L]
     const double* tw;        // ph_f tables [L][n]
@@ -314,26 +210,31 @@ __global__ __launch_bounds__(256) void enc_ring_kernel(RingArgs ra, const uint64
     const uint64_t Rc = live ? R : 0;
     const uint64_t y = Rc % N;
     const uint32_t wl = (uint32_t)(Rc / N), w = wl / (uint32_t)ra.L, l = wl - w * (uint32_t)ra.L;   // wl < 2^32
-    const uint64_t i0 = Rc * N + 4 * j;                                  // matrix-major
-    const uint64_t p0 = (((uint64_t)w * N + y) * ra.L + l) * N + 4 * j;  // poly-major
+    constexpr bool LDS = LOGN == 6 && MFHE_RING_LDS;   // ring_mul_row64_lds: reg s holds coefficient j + 16 s
+    const uint64_t i0 = Rc * N, p0 = (((uint64_t)w * N + y) * ra.L + l) * N;   // row starts: matrix- / poly-major
     const LimbConst lc = ra.lf[l];
     const ArithF64 ar(lc);
     uint64_t av[4], sk[4];
-    ld4(aev + p0, av);
+    ld_row<LDS>(aev + p0, j, av);
     ld4(ra.sk + ((uint64_t)w * ra.L + l) * N + 4 * j, sk);
     // the combine's operands are loaded before the ring product (clamped rows for dead lanes), so their latency
     // overlaps the butterflies instead of following them
     uint64_t ev[4], mv[4], mi[4], b[4];
-    ld4(e + p0, ev);
-    ld4(m_re + i0, mv);
-    if (m_im) ld4(m_im + i0, mi);
+    ld_row<LDS>(e + p0, j, ev);
+    ld_row<LDS>(m_re + i0, j, mv);
+    if (m_im) ld_row<LDS>(m_im + i0, j, mi);
     double x[4], sv[4];
 #pragma unroll
     for (int s = 0; s < 4; ++s) {
         x[s] = ArithF64::from_u64(av[s]);
         sv[s] = centred_f(sk[s], lc.qf);
     }
-    ring_mul_row<LOGN>(x, sv, j, ar, ra.tw + l * N, ra.itw + l * N, ra.ninv[l]);
+    if constexpr (LDS) {
+        __shared__ double rscr[16 * 68];
+        ring_mul_row64_lds(x, sv, j, ar, ra.tw + l * N, ra.itw + l * N, ra.ninv[l], rscr + (threadIdx.x >> 4) * 68);
+    } else {
+        ring_mul_row<LOGN>(x, sv, j, ar, ra.tw + l * N, ra.itw + l * N, ra.ninv[l]);
+    }
     if (!live) return;
     const uint64_t q = lc.q, total = ra.rows * N;
     auto bval = [&](uint64_t m, int s) {
@@ -344,13 +245,13 @@ __global__ __launch_bounds__(256) void enc_ring_kernel(RingArgs ra, const uint64
     };
 #pragma unroll
     for (int s = 0; s < 4; ++s) b[s] = bval(mv[s], s);
-    st4(ct_re + i0, b);
-    st4(ct_re + total + i0, av);
+    st_row<LDS>(ct_re + i0, j, b);
+    st_row<LDS>(ct_re + total + i0, j, av);
     if (m_im) {
 #pragma unroll
         for (int s = 0; s < 4; ++s) b[s] = bval(mi[s], s);
-        st4(ct_im + i0, b);
-        st4(ct_im + total + i0, av);
+        st_row<LDS>(ct_im + i0, j, b);
+        st_row<LDS>(ct_im + total + i0, j, av);
     }
 }
 
@@ -367,28 +268,34 @@ __global__ __launch_bounds__(256) void dec_ring_kernel(RingArgs ra, const uint64
     const uint64_t Rc = live ? R : 0;
     const uint64_t y = Rc % N;
     const uint32_t wl = (uint32_t)(Rc / N), w = wl / (uint32_t)ra.L, l = wl - w * (uint32_t)ra.L;   // wl < 2^32
-    const uint64_t i0 = Rc * N + 4 * j, total = ra.rows * N;
-    const uint64_t p0 = (((uint64_t)w * N + y) * ra.L + l) * N + 4 * j;
+    constexpr bool LDS = LOGN == 6 && MFHE_RING_LDS;   // as enc_ring_kernel
+    const uint64_t i0 = Rc * N, total = ra.rows * N;
+    const uint64_t p0 = (((uint64_t)w * N + y) * ra.L + l) * N;
     const LimbConst lc = ra.lf[l];
     const ArithF64 ar(lc);
     uint64_t av[4], sk[4], bv[4];
-    ld4(ct + total + i0, av);
+    ld_row<LDS>(ct + total + i0, j, av);
     ld4(ra.sk + ((uint64_t)w * ra.L + l) * N + 4 * j, sk);
-    ld4(ct + i0, bv);   // before the ring product, so its latency overlaps the butterflies (clamped row if dead)
+    ld_row<LDS>(ct + i0, j, bv);   // before the ring product, so its latency overlaps the butterflies (clamped row if dead)
     double x[4], sv[4];
 #pragma unroll
     for (int s = 0; s < 4; ++s) {
         x[s] = ArithF64::from_u64(av[s]);
         sv[s] = centred_f(sk[s], lc.qf);
     }
-    ring_mul_row<LOGN>(x, sv, j, ar, ra.tw + l * N, ra.itw + l * N, ra.ninv[l]);
+    if constexpr (LDS) {
+        __shared__ double rscr[16 * 68];
+        ring_mul_row64_lds(x, sv, j, ar, ra.tw + l * N, ra.itw + l * N, ra.ninv[l], rscr + (threadIdx.x >> 4) * 68);
+    } else {
+        ring_mul_row<LOGN>(x, sv, j, ar, ra.tw + l * N, ra.itw + l * N, ra.ninv[l]);
+    }
     if (!live) return;
 #pragma unroll
     for (int s = 0; s < 4; ++s) {
         const uint64_t sum = bv[s] + ar.canon(x[s]);
         bv[s] = sum >= lc.q ? sum - lc.q : sum;
     }
-    st4(out + p0, bv);
+    st_row<LDS>(out + p0, j, bv);
 }
 
 static bool ring_fused_ok(const mfhe_ctx* c, int logn) {
@@ -405,6 +312,13 @@ static RingArgs ring_args(const mfhe_ctx* c, const uint64_t* sk, int L, uint64_t
     ra.L = L;
     ra.rows = rows;
     return ra;
+}
+
+// decrypt_and_decode: the decrypt fused into the factored inverse W-CRT's digitize (n = 64, the same conditions
+// as the factored inverse in use_mfma plus ring_fused_ok)
+static bool dec_fused_ok(const mfhe_ctx* c, int logn) {
+    return ring_fused_ok(c, logn) && logn == 6 && c->wcrt_mfma == 1 && c->wD && c->d_wZidig && c->d_wepi &&
+           c->d_wifold && c->d_wiz && c->d_wphi;
 }
 
 #define MFHE_RING_DISPATCH(KERNEL, logn, grid, s, ...)                                       \
@@ -618,7 +532,8 @@ static bool quant_fused_ok(const mfhe_ctx* c) {
     return c->wcrt_mfma == 1 && c->wD && c->d_wZdig && c->d_wepi && c->d_wfold;
 }
 static int wcrt_gemm(mfhe_ctx* c, const uint64_t* A, const uint64_t* B, bool b_poly, uint64_t* C, WOut out,
-                     bool vector, hipStream_t s, int qsrc = 0, const double* qf = nullptr, uint64_t qf_step = 1) {
+                     bool vector, hipStream_t s, int qsrc = 0, const double* qf = nullptr, uint64_t qf_step = 1,
+                     const RingArgs* dec = nullptr) {
     const Geo2 g = geo(c);
     ModGemmArgs a;
     a.A = A;
@@ -642,6 +557,18 @@ static int wcrt_gemm(mfhe_ctx* c, const uint64_t* A, const uint64_t* B, bool b_p
         else { a.cL = g.n2; a.scM = (uint64_t)g.L * g.n2; a.scY = g.n; }
     }
     RC(use_mfma(c, a, A, g.L));
+    if (dec) {
+        // B is the ciphertext: the factored inverse's digitize decrypts it row by row (gemm.hip
+        // mfma_digitize_ifold_dec_kernel); only where dec_fused_ok(c)
+        if (!a.ifold) return set_error(MFHE_EINVAL, "W-CRT: a decrypt-fused source needs the factored inverse");
+        a.dct = B;
+        a.dtotal = g.words;
+        a.dsk = dec->sk;
+        a.dlf = dec->lf;
+        a.dtw = dec->tw;
+        a.ditw = dec->itw;
+        a.dninv = dec->ninv;
+    }
     if (qsrc) {
         if (!a.fold) return set_error(MFHE_EINVAL, "W-CRT: a fused digitize source needs the factored forward");
         a.qsrc = qsrc;
@@ -755,8 +682,9 @@ static int encode_impl(mfhe_ctx* c, const double* msg, uint64_t* out_re, uint64_
     return MFHE_OK;
 }
 
+// dec: ev_re / ev_im are the ciphertexts, decrypted inside the W-INTT's digitize (dec_fused_ok only)
 static int decode_impl(mfhe_ctx* c, const uint64_t* ev_re, const uint64_t* ev_im, double* msg, hipStream_t s,
-                       Bump* pb = nullptr) {
+                       Bump* pb = nullptr, const RingArgs* dec = nullptr) {
     RC(need_wcrt(c));
     if (!ev_re || !ev_im || !msg) return set_error(MFHE_EINVAL, "mfhe_decode: null pointer");
     RC(ensure_xy(c));
@@ -770,9 +698,9 @@ static int decode_impl(mfhe_ctx* c, const uint64_t* ev_re, const uint64_t* ev_im
     double2* ccx = pb->get<double2>(g.cnt);
     double2* ecx = pb->get<double2>(g.cnt);
     // W-INTT (poly-major in -> matrix-major coeff), CRT compose + centre + /delta fused, into re / im
-    RC(wcrt_gemm(c, c->d_wVinv, ev_re, true, coeff, WOut::Matrix, false, s));
+    RC(wcrt_gemm(c, c->d_wVinv, ev_re, true, coeff, WOut::Matrix, false, s, 0, nullptr, 1, dec));
     RC(mfhe_crt_compose_f64(c, coeff, 512, g.n2, (double*)ccx, 2, (mfhe_stream_t)s));
-    RC(wcrt_gemm(c, c->d_wVinv, ev_im, true, coeff, WOut::Matrix, false, s));
+    RC(wcrt_gemm(c, c->d_wVinv, ev_im, true, coeff, WOut::Matrix, false, s, 0, nullptr, 1, dec));
     RC(mfhe_crt_compose_f64(c, coeff, 512, g.n2, (double*)ccx + 1, 2, (mfhe_stream_t)s));
     // W-DFT, then XY-DFT per lane: M = V E V^T
     RC(wdft(c, c->d_wdV, ccx, ecx, s));
@@ -878,7 +806,8 @@ static int decrypt_impl(mfhe_ctx* c, const uint64_t* ct, const uint64_t* sk, uin
 // f64 slices, then the W-DFT and XY-DFT of the whole batch (FP64, replicated on every rank).  Replaces
 // decode_eval_pair_to_complex (HE.cu:1619-1689) whose per-lane compose loop (:1653-1668) is the exchange step.
 static int decode_sharded_impl(mfhe_ctx* c, mfhe_ctx* call, mfhe_comm* comm, int mode, const uint64_t* ev_re,
-                               const uint64_t* ev_im, double* msg, hipStream_t s, Bump* pb) {
+                               const uint64_t* ev_im, double* msg, hipStream_t s, Bump* pb,
+                               const RingArgs* dec = nullptr) {
     const Geo2 g = geo(c);
     int G = 1, rank = 0;
     RC(comm_size_rank(comm, &G, &rank));
@@ -891,8 +820,8 @@ static int decode_sharded_impl(mfhe_ctx* c, mfhe_ctx* call, mfhe_comm* comm, int
     // lane index (MFHE_RECOMBINE_ROWS_GLOBAL), so each chunk's lanes [p0, p0 + cp) are [rank][cp / G] in lane order
     // and one in-place all-gather per chunk completes them on every rank.
     const size_t cp = mfhe_ctx::PHI / 4 >= (size_t)G ? mfhe_ctx::PHI / 4 / G * G : (size_t)G;
-    RC(wcrt_gemm(c, c->d_wVinv, ev_re, true, coeff_re, WOut::Matrix, false, s));
-    RC(wcrt_gemm(c, c->d_wVinv, ev_im, true, coeff_im, WOut::Matrix, false, s));
+    RC(wcrt_gemm(c, c->d_wVinv, ev_re, true, coeff_re, WOut::Matrix, false, s, 0, nullptr, 1, dec));
+    RC(wcrt_gemm(c, c->d_wVinv, ev_im, true, coeff_im, WOut::Matrix, false, s, 0, nullptr, 1, dec));
     RC(mfhe_crt_recombine_chunked(call, comm, mode, coeff_re, 512, g.n2, cp, (double*)ccx, 2,
                                   MFHE_RECOMBINE_ROWS_GLOBAL, (mfhe_stream_t)s));
     RC(mfhe_crt_recombine_chunked(call, comm, mode, coeff_im, 512, g.n2, cp, (double*)ccx + 1, 2,
@@ -1049,6 +978,10 @@ extern "C" int mfhe_decrypt_and_decode(mfhe_ctx* c, const uint64_t* cre, const u
     RC(ensure_ws(c));
     const Geo2 g = geo(c);
     Bump b{(char*)c->ws};
+    if (dec_fused_ok(c, g.logn)) {
+        const RingArgs ra = ring_args(c, sk, g.L, g.words / g.n);
+        return decode_impl(c, cre, cim, msg, (hipStream_t)s, &b, &ra);
+    }
     uint64_t* er = b.get<uint64_t>(g.words);
     uint64_t* ei = b.get<uint64_t>(g.words);
     Bump inner = b;
@@ -1100,6 +1033,10 @@ extern "C" int mfhe_decrypt_and_decode_sharded(mfhe_ctx* c, mfhe_ctx* call, mfhe
     RC(comm_agree(comm, rc, (hipStream_t)s));
     const Geo2 g = geo(c);
     Bump b{(char*)c->ws};
+    if (dec_fused_ok(c, g.logn)) {
+        const RingArgs ra = ring_args(c, sk, g.L, g.words / g.n);
+        return decode_sharded_impl(c, call, comm, mode, cre, cim, msg, (hipStream_t)s, &b, &ra);
+    }
     uint64_t* er = b.get<uint64_t>(g.words);
     uint64_t* ei = b.get<uint64_t>(g.words);
     Bump inner = b;

@@ -339,7 +339,9 @@ def _encrypt_decrypt_vs_oracle(mfhe, orc, n, ctx, h, moduli):
 @pytest.mark.parametrize("n,L", [(4, 2), (8, 11), (16, 3), (64, 11)])
 def test_fused_ring_matches_unfused(mfhe, n, L):
     """encrypt_pair / decrypt_to_eval with the fused X-NTT * s * X-INTT row kernels (he.hip enc_ring_kernel,
-    dec_ring_kernel; MFHE_OPT_HE_FUSED = 1, default) == the separate NTT / pointwise / combine kernels, bit-exact."""
+    dec_ring_kernel; MFHE_OPT_HE_FUSED = 1, default) == the separate NTT / pointwise / combine kernels, bit-exact.
+    decrypt_and_decode too: at n = 64 the fused path decrypts inside the inverse W-CRT's digitize (gemm.hip
+    mfma_digitize_ifold_dec_kernel), the unfused one through decrypt_to_eval and the plain digitize."""
     import torch
     ctx = mfhe.Context(RNS[:L], n.bit_length() - 1, CONV)
     assert ctx.get_option(mfhe.OPT_HE_FUSED) == 1
@@ -356,8 +358,10 @@ def test_fused_ring_matches_unfused(mfhe, n, L):
         ctx.encrypt_pair(_dev(mfhe, m_re), _dev(mfhe, m_im), sk, cre, cim)
         ev = torch.empty(words, dtype=torch.int64, device="cuda")
         ctx.decrypt_to_eval(cre, sk, ev)
+        msg = torch.empty(2 * 512 * n * n, dtype=torch.float64, device="cuda")
+        ctx.decrypt_and_decode(cre, cim, sk, msg)
         torch.cuda.synchronize()
-        res[mode] = [mfhe.to_host_u64(t) for t in (cre, cim, ev)]
+        res[mode] = [mfhe.to_host_u64(t) for t in (cre, cim, ev)] + [msg.cpu().numpy()]
     for a, b in zip(res[1], res[0]):
         np.testing.assert_array_equal(a, b)
     # decrypt(encrypt(m)) = m + e: small noise around the message in the coefficient domain is checked by

@@ -102,6 +102,7 @@ def test_column_pass_dma_waits_match_the_instruction_mix(inv, arith):
     r"_ZN4mfhe25mfma_digitize_fold_kernelILi5ELi1E[^>]*",
     r"_ZN4mfhe25mfma_digitize_fold_kernelILi5ELi3E[^>]*",
     r"_ZN4mfhe26mfma_digitize_ifold_kernelILi5E[^>]*",
+    r"_ZN4mfhe30mfma_digitize_ifold_dec_kernelILi6E[^>]*",
 ])
 def test_digitize_loads_are_not_serialised(kernel):
     """The W-CRT digitize kernels (gemm.hip) must keep their column loads in flight together: a load under a
