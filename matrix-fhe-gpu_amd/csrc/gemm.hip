@@ -3,6 +3,10 @@
 #include "mfhe_ctx.hpp"
 #include "ring_row.hpp"
 
+#ifndef MFHE_DEC_SPLIT
+#define MFHE_DEC_SPLIT 4   // decrypt-fused digitize: workgroups per (row, limb), each 8 / MFHE_DEC_SPLIT panels
+#endif
+
 namespace mfhe {
 
 using u128 = unsigned __int128;
@@ -748,6 +752,26 @@ __global__ __launch_bounds__(256) void mfma_digitize_ifold_kernel(ModGemmArgs a,
     }
 }
 
+// rows r2 = 0, 255, 256 of the factored inverse from the column sums E_a'[0], E_a'[255], E_a'[256] (a = 1: e1,
+// a = 2: e2), as at the end of mfma_digitize_ifold_kernel: f_0 and f_257 into C, (c0, c1) into cc
+template <class FO>
+__device__ __forceinline__ void ifold_finish(const ModGemmArgs& a, const ArithF64& ar, FO fo, const double (&e1)[3],
+                                             const double (&e2)[3], int l, uint32_t Ppad, uint32_t p) {
+    const double h0 = ar.mulmod(e1[0], fo[2]) + ar.mulmod(e2[0], fo[5]);
+    const double h257 = ar.mulmod(e1[0], fo[8]) + ar.mulmod(e2[0], fo[11]);
+    const double h512 = ar.mulmod(e1[1], fo[8]) + ar.mulmod(e2[1], fo[11]);
+    const double h513 = ar.mulmod(e1[2], fo[9]) + ar.mulmod(e2[2], fo[12]);
+    auto phi = [&](int byte, int sh) { return (double)((int)((a.phi[byte] >> sh) & 3) - 1); };
+    const double c1 = ar.reduce(h513);
+    const double c0 = ar.reduce(h512 - c1 * phi(254, 6));
+    const uint32_t nmask = (1u << a.log_n) - 1;
+    uint64_t* Cl = a.C + (uint64_t)l * a.cL + (uint64_t)(p >> a.log_n) * a.scY + (p & nmask);
+    Cl[0] = ar.canon(h0 - c0 * phi(256, 0));
+    Cl[257 * a.scM] = ar.canon(h257 - c0 * phi(256, 4) - c1 * phi(256, 6));
+    a.cc[((uint64_t)l * Ppad + p) * 2] = c0;
+    a.cc[((uint64_t)l * Ppad + p) * 2 + 1] = c1;
+}
+
 // The same digitize with the decrypt fused in front of it (n = 64, he.hip mfhe_decrypt_and_decode): B is never
 // written to HBM.  One workgroup owns limb l and row y: the 64 columns p = 64 y + x over all 512 k (= w), so the
 // whole X row of every (w, l, y) -- what the ring product needs -- is inside the workgroup, and the column sums
@@ -788,8 +812,9 @@ __global__ __launch_bounds__(256) void mfma_digitize_ifold_dec_kernel(ModGemmArg
     double s0 = 0.0, s1 = 0.0, s2 = 0.0;
     // all four substeps' loads are issued before the first ring product (measured: a one-substep-ahead rolling
     // prefetch needs 186 VGPRs, 2 workgroups per CU, or spills at 3: 2-5% slower, profiles/r04_dec_fused_ab.txt)
+    const int kpg = FK / 32 / (int)gridDim.z, kc0 = blockIdx.z * kpg;   // this block's share of the panels
 #pragma unroll 1
-    for (int kc = 0; kc < FK / 32; ++kc) {
+    for (int kc = kc0; kc < kc0 + kpg; ++kc) {
         uint64_t av[4][4], sk[4][4], bv[4][4];
 #pragma unroll
         for (int st = 0; st < 4; ++st) {
@@ -867,6 +892,15 @@ __global__ __launch_bounds__(256) void mfma_digitize_ifold_dec_kernel(ModGemmArg
     bt[(1 * 4 + wv) * 64 + lane] = s1;
     bt[(2 * 4 + wv) * 64 + lane] = s2;
     __syncthreads();
+    if (gridDim.z > 1) {
+        // a share of the panels: this block's sums per (column, a') to the partials, finished by dec_colsum_kernel
+        if (wv >= 2) return;
+        double* o = a.dpart + (((uint64_t)blockIdx.z * L + l) * Ppad + p) * 6 + wv * 3;
+#pragma unroll
+        for (int tt = 0; tt < 3; ++tt)
+            o[tt] = ar.reduce(bt[(tt * 4 + 2 * wv) * 64 + lane] + bt[(tt * 4 + 2 * wv + 1) * 64 + lane]);
+        return;
+    }
     if (wv != 0) return;
     double e1[3], e2[3];   // a = 1 (a' = 0), a = 2 (a' = 1)
 #pragma unroll
@@ -874,18 +908,33 @@ __global__ __launch_bounds__(256) void mfma_digitize_ifold_dec_kernel(ModGemmArg
         e1[tt] = ar.reduce(bt[(tt * 4 + 0) * 64 + lane] + bt[(tt * 4 + 1) * 64 + lane]);
         e2[tt] = ar.reduce(bt[(tt * 4 + 2) * 64 + lane] + bt[(tt * 4 + 3) * 64 + lane]);
     }
-    const double h0 = ar.mulmod(e1[0], fo[2]) + ar.mulmod(e2[0], fo[5]);
-    const double h257 = ar.mulmod(e1[0], fo[8]) + ar.mulmod(e2[0], fo[11]);
-    const double h512 = ar.mulmod(e1[1], fo[8]) + ar.mulmod(e2[1], fo[11]);
-    const double h513 = ar.mulmod(e1[2], fo[9]) + ar.mulmod(e2[2], fo[12]);
-    auto phi = [&](int byte, int sh) { return (double)((int)((a.phi[byte] >> sh) & 3) - 1); };
-    const double c1 = ar.reduce(h513);
-    const double c0 = ar.reduce(h512 - c1 * phi(254, 6));
-    uint64_t* Cl = a.C + (uint64_t)l * a.cL + (uint64_t)y * a.scY + lane;
-    Cl[0] = ar.canon(h0 - c0 * phi(256, 0));
-    Cl[257 * a.scM] = ar.canon(h257 - c0 * phi(256, 4) - c1 * phi(256, 6));
-    a.cc[((uint64_t)l * Ppad + p) * 2] = c0;
-    a.cc[((uint64_t)l * Ppad + p) * 2 + 1] = c1;
+    ifold_finish(a, ar, fo, e1, e2, l, Ppad, p);
+}
+
+// the column sums of a split decrypt-fused digitize (gridDim.z = G shares of the panels): one thread per (column, limb)
+__global__ __launch_bounds__(256) void dec_colsum_kernel(ModGemmArgs a, uint32_t Ppad, int G) {
+    const uint32_t p = blockIdx.x * 256 + threadIdx.x;
+    const int l = blockIdx.y, L = gridDim.y;
+    if (p >= Ppad) return;
+    typedef const __attribute__((address_space(4))) double* cdp_t;
+    const cdp_t fo = (cdp_t)(a.ifold + (uint64_t)l * 16);
+    LimbConst lc;
+    lc.qf = fo[0];
+    lc.qinv = fo[1];
+    const ArithF64 ar(lc);
+    double e[6] = {0, 0, 0, 0, 0, 0};
+    for (int g = 0; g < G; ++g) {   // |partial| <= q / 2: G <= 8 terms stay exact
+        const double* o = a.dpart + (((uint64_t)g * L + l) * Ppad + p) * 6;
+#pragma unroll
+        for (int t = 0; t < 6; ++t) e[t] += o[t];
+    }
+    double e1[3], e2[3];
+#pragma unroll
+    for (int tt = 0; tt < 3; ++tt) {
+        e1[tt] = ar.reduce(e[tt]);
+        e2[tt] = ar.reduce(e[3 + tt]);
+    }
+    ifold_finish(a, ar, fo, e1, e2, l, Ppad, p);
 }
 
 // C = sum_s acc_s * 256^s mod q for the 32 x 32 wave tile at (m0, p0) of limb l (lane = (r, h)).
@@ -1342,7 +1391,8 @@ static void launch_staged(int pipe, dim3 grid, hipStream_t s, const ModGemmArgs&
 
 size_t mod_gemm_mfma_ws(uint32_t P, int L, int D) {
     const uint64_t Ppad = ((uint64_t)P + 63) / 64 * 64;
-    return (size_t)L * D * Ppad * MK + (size_t)L * 2 * Ppad * 8;   // digit planes, then the factored d0
+    // digit planes, then the factored d0 / (c0, c1), then the split decrypt-fused digitize's column partials
+    return (size_t)L * D * Ppad * MK + (size_t)L * 2 * Ppad * 8 + (size_t)MFHE_DEC_SPLIT * L * Ppad * 6 * 8;
 }
 
 void balanced_digits(uint64_t x, int D, int8_t* out) {
@@ -1418,10 +1468,18 @@ static int launch_factored_inv(const ModGemmArgs& a, int L, hipStream_t s) {
         // decrypt fused (n = 64 rows: one workgroup per (y, l), 64 columns)
         if (a.log_n != 6 || a.P != 64u * 64u || Ppad != a.P || !a.dsk || !a.dlf || !a.dtw || !a.ditw || !a.dninv)
             return set_error(MFHE_EINVAL, "mod_gemm: the decrypt-fused inverse W-CRT needs n = 64 and the ring tables");
-        const dim3 gr(64, L);
+        // MFHE_DEC_SPLIT workgroups per (row, limb), each a share of the 8 panels, the column sums finished after
+        constexpr int G = MFHE_DEC_SPLIT;
+        static_assert(G == 1 || G == 2 || G == 4 || G == 8, "the 8 panels split evenly");
+        f.dpart = f.cc + (size_t)L * Ppad * 2;
+        const dim3 gr(64, L, G);
         if (a.D == 5) hipLaunchKernelGGL(mfma_digitize_ifold_dec_kernel<5>, gr, dim3(256), 0, s, f, Ppad, pc);
         else hipLaunchKernelGGL(mfma_digitize_ifold_dec_kernel<6>, gr, dim3(256), 0, s, f, Ppad, pc);
         MFHE_CHECK_LAUNCH("mfma_digitize_ifold_dec_kernel");
+        if (G > 1) {
+            hipLaunchKernelGGL(dec_colsum_kernel, dim3((Ppad + 255) / 256, L), dim3(256), 0, s, f, Ppad, G);
+            MFHE_CHECK_LAUNCH("dec_colsum_kernel");
+        }
     } else {
         const dim3 gd(Ppad / 16, L);
         if (a.D == 5) hipLaunchKernelGGL(mfma_digitize_ifold_kernel<5>, gd, dim3(256), 0, s, f, Ppad, pc);

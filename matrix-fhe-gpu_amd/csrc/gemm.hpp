@@ -70,6 +70,7 @@ struct ModGemmArgs {
     const double* dtw = nullptr;      // X-NTT tables [L][n] (ph_f)
     const double* ditw = nullptr;
     const double* dninv = nullptr;    // [L]
+    double* dpart = nullptr;          // set by the launcher: [G][L][Ppad][6] column partials of a split launch
 };
 
 // bytes of B digit workspace the MFMA path needs for P columns and L limbs at D digits
