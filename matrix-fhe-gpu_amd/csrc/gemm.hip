@@ -3,6 +3,15 @@
 #include "mfhe_ctx.hpp"
 #include "ring_row.hpp"
 
+#ifndef MFHE_DEC_WG_CU
+#define MFHE_DEC_WG_CU 1   // decrypt-fused digitize: minimum workgroups per CU for the register budget (A/B knob)
+#endif
+#ifndef MFHE_DEC_TW_LDS
+#define MFHE_DEC_TW_LDS 0   // decrypt-fused digitize: ring twiddles read from LDS (A/B knob)
+#endif
+#ifndef MFHE_DEC_SUBS
+#define MFHE_DEC_SUBS 4   // decrypt-fused digitize: 16-row substeps loaded together (1, 2 or 4)
+#endif
 #ifndef MFHE_DEC_SPLIT
 #define MFHE_DEC_SPLIT 4   // decrypt-fused digitize: workgroups per (row, limb), each 8 / MFHE_DEC_SPLIT panels
 #endif
@@ -783,7 +792,7 @@ __device__ __forceinline__ void ifold_finish(const ModGemmArgs& a, const ArithF6
 // Reads: ct (16 B per element) + s (L2-resident); writes: the digit planes.  The B round trip of the unfused path
 // (8 B written by dec_ring_kernel + 8 B read here per element) and one launch per component are gone.
 template <int D>
-__global__ __launch_bounds__(256) void mfma_digitize_ifold_dec_kernel(ModGemmArgs a, uint32_t Ppad, PlaneCounts pc) {
+__global__ __launch_bounds__(256, MFHE_DEC_WG_CU) void mfma_digitize_ifold_dec_kernel(ModGemmArgs a, uint32_t Ppad, PlaneCounts pc) {
     constexpr int LOGN = 6, N = 64, RS = N + 2;   // row stride 528 B: the ring's 16-B row writes spread over banks
     __shared__ __attribute__((aligned(16))) double bt[64 * RS];
     const int t = threadIdx.x, lane = t & 63, wv = t >> 6;
@@ -803,8 +812,18 @@ __global__ __launch_bounds__(256) void mfma_digitize_ifold_dec_kernel(ModGemmArg
     const int nd = l < 64 ? pc.n[l] : D;
     // ring-stage lane: 4 coefficients 4 j .. 4 j + 3 of row 16 s + rs (s = 0..3)
     const int j = t & 15, rs = t >> 4;
+#if MFHE_DEC_TW_LDS
+    // the limb's X-NTT tables in LDS: read per butterfly inside the panel loop instead of held in ~40 VGPRs
+    __shared__ double twl[2 * N];
+    if (t < N) twl[t] = a.dtw[(uint64_t)l * N + t];
+    else if (t < 2 * N) twl[t] = a.ditw[(uint64_t)l * N + t - N];
+    __syncthreads();
+    const double* tw = twl;
+    const double* itw = twl + N;
+#else
     const double* tw = a.dtw + (uint64_t)l * N;
     const double* itw = a.ditw + (uint64_t)l * N;
+#endif
     const double ninv = a.dninv[l];
     // digitize-stage lane: column x = lane, (a', hf) = wave
     const int ap = wv >> 1, hf = wv & 1;
@@ -815,35 +834,40 @@ __global__ __launch_bounds__(256) void mfma_digitize_ifold_dec_kernel(ModGemmArg
     const int kpg = FK / 32 / (int)gridDim.z, kc0 = blockIdx.z * kpg;   // this block's share of the panels
 #pragma unroll 1
     for (int kc = kc0; kc < kc0 + kpg; ++kc) {
-        uint64_t av[4][4], sk[4][4], bv[4][4];
 #pragma unroll
-        for (int st = 0; st < 4; ++st) {
+        for (int sb = 0; sb < 4; sb += MFHE_DEC_SUBS) {   // MFHE_DEC_SUBS substeps' loads in flight together
+        uint64_t av[MFHE_DEC_SUBS][4], sk[MFHE_DEC_SUBS][4], bv[MFHE_DEC_SUBS][4];
+#pragma unroll
+        for (int si = 0; si < MFHE_DEC_SUBS; ++si) {
+            const int st = sb + si;
             const int rr = st * 16 + rs;
             const uint64_t w = (uint64_t)(rr >> 5) * FK + kc * 32 + (rr & 31);
             const uint64_t wl = w * L + l, r0 = (wl * N + y) * N;
-            ld4(a.dct + a.dtotal + r0 + 4 * j, av[st]);
-            ld4(a.dsk + wl * N + 4 * j, sk[st]);
-            ld4(a.dct + r0 + 4 * j, bv[st]);
+            ld4(a.dct + a.dtotal + r0 + 4 * j, av[si]);
+            ld4(a.dsk + wl * N + 4 * j, sk[si]);
+            ld4(a.dct + r0 + 4 * j, bv[si]);
         }
         // ring product per row (the shuffle ring_mul_row: ring_mul_row64_lds measured slower here, 198 vs 183 us)
 #pragma unroll
-        for (int st = 0; st < 4; ++st) {
+        for (int si = 0; si < MFHE_DEC_SUBS; ++si) {
+            const int st = sb + si;
             double x[4], sv[4];
 #pragma unroll
             for (int e = 0; e < 4; ++e) {
-                x[e] = ArithF64::from_u64(av[st][e]);
-                sv[e] = centred_f(sk[st][e], rl.qf);
+                x[e] = ArithF64::from_u64(av[si][e]);
+                sv[e] = centred_f(sk[si][e], rl.qf);
             }
             ring_mul_row<LOGN>(x, sv, j, rar, tw, itw, ninv);
             double v[4];
 #pragma unroll
             for (int e = 0; e < 4; ++e) {
-                const uint64_t sum = bv[st][e] + rar.canon(x[e]);
+                const uint64_t sum = bv[si][e] + rar.canon(x[e]);
                 v[e] = ar.reduce(ArithF64::from_u64(sum >= rl.q ? sum - rl.q : sum));
             }
             double* row = bt + (st * 16 + rs) * RS + 4 * j;
             *(double2*)row = make_double2(v[0], v[1]);
             *(double2*)(row + 2) = make_double2(v[2], v[3]);
+        }
         }
         __syncthreads();
         const int k0 = kc * 32 + hf * 16;
