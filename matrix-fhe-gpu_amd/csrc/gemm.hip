@@ -9,6 +9,9 @@
 #ifndef MFHE_DEC_TW_LDS
 #define MFHE_DEC_TW_LDS 0   // decrypt-fused digitize: ring twiddles read from LDS (A/B knob)
 #endif
+#ifndef MFHE_DEC_RING_C
+#define MFHE_DEC_RING_C 0   // decrypt-fused digitize: 1 = ring_mul_row64_lds from layout-C loads (A/B knob)
+#endif
 #ifndef MFHE_DEC_SUBS
 #define MFHE_DEC_SUBS 4   // decrypt-fused digitize: 16-row substeps loaded together (1, 2 or 4)
 #endif
@@ -795,6 +798,9 @@ template <int D>
 __global__ __launch_bounds__(256, MFHE_DEC_WG_CU) void mfma_digitize_ifold_dec_kernel(ModGemmArgs a, uint32_t Ppad, PlaneCounts pc) {
     constexpr int LOGN = 6, N = 64, RS = N + 2;   // row stride 528 B: the ring's 16-B row writes spread over banks
     __shared__ __attribute__((aligned(16))) double bt[64 * RS];
+#if MFHE_DEC_RING_C
+    __shared__ double rscr[16 * 68];   // ring_mul_row64_lds transposes, one row per 16 lanes
+#endif
     const int t = threadIdx.x, lane = t & 63, wv = t >> 6;
     const uint32_t y = blockIdx.x;
     const int l = blockIdx.y, L = gridDim.y;
@@ -857,7 +863,22 @@ __global__ __launch_bounds__(256, MFHE_DEC_WG_CU) void mfma_digitize_ifold_dec_k
                 x[e] = ArithF64::from_u64(av[si][e]);
                 sv[e] = centred_f(sk[si][e], rl.qf);
             }
+#if MFHE_DEC_RING_C
+            // ring_mul_row64_lds from 32-byte layout-C loads (one extra transpose in); b in layout C too, so the
+            // product comes back to C through the row scratch before the add
+            ring_mul_row64_lds<true>(x, sv, j, rar, tw, itw, ninv, rscr + rs * 68);
+            {
+                double* scr = rscr + rs * 68;
+#pragma unroll
+                for (int e = 0; e < 4; ++e) scr[(j + 16 * e) + ((j + 16 * e) >> 4)] = x[e];
+                asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+#pragma unroll
+                for (int e = 0; e < 4; ++e) x[e] = scr[(4 * j + e) + ((4 * j + e) >> 4)];
+                asm volatile("" ::: "memory");
+            }
+#else
             ring_mul_row<LOGN>(x, sv, j, rar, tw, itw, ninv);
+#endif
             double v[4];
 #pragma unroll
             for (int e = 0; e < 4; ++e) {

@@ -113,6 +113,8 @@ __device__ __forceinline__ void ring_mul_row(double (&x)[4], const double (&sv)[
 // schedule too), so the canonical outputs are identical.  In and out in layout A; s in layout C.  The 16 lanes of
 // a row are in one wave: the transposes need no barrier, only the wave's in-order LDS (the compiler is held by
 // the memory clobbers).
+// IN_C: x arrives in layout C (4 j + m, one 32-byte load per lane) and is transposed to A first.
+template <bool IN_C = false>
 __device__ __forceinline__ void ring_mul_row64_lds(double (&x)[4], const double (&sv)[4], int j, const ArithF64& ar,
                                                    const double* __restrict__ tw, const double* __restrict__ itw,
                                                    double ninv, double* scr) {
@@ -141,6 +143,7 @@ __device__ __forceinline__ void ring_mul_row64_lds(double (&x)[4], const double 
         for (int m = 0; m < 4; ++m) x[m] = scr[slot(rs + rstep * m)];
         asm volatile("" ::: "memory");   // the next transpose's writes stay behind these reads
     };
+    if constexpr (IN_C) xchg(sC, 1, sA, 16);
     // forward (CT, W = tw[m + e / 2t])
     ct(0, 2, tw[1]);
     ct(1, 3, tw[1]);
