@@ -1,0 +1,9 @@
+# r04 closing check at HEAD: the whole GPU suite, smoke(), the driver's default bench command
+set -o pipefail
+O=gpurun_out/r04ae; mkdir -p $O
+timeout -k 10 600 python3 -u -m pytest tests -m gpu -x -q --timeout 300 --timeout-method thread > $O/pytest_gpu.log 2>&1 || { tail -30 $O/pytest_gpu.log; exit 1; }
+tail -1 $O/pytest_gpu.log
+timeout -k 10 300 python3 -c "import __graft_entry__ as g; g.smoke()" > $O/smoke.log 2>&1 || { tail -20 $O/smoke.log; exit 9; }
+tail -1 $O/smoke.log
+timeout -k 10 400 python3 bench.py > $O/bench.json 2> $O/bench.err || { tail -20 $O/bench.err; exit 3; }
+python3 -c "import json; d=json.load(open('$O/bench.json')); print(d['value'], d['roofline']['frac'], d['reference_geometry_pipeline']['ms'], d['c4_sharded_pipeline']['allgather']['ms'])"
