@@ -315,6 +315,35 @@ def trace_line(reps=10):
             "modmul_kernel_gemm_ms": round(m_ms, 3), "split_valu_kernel_gemm_ms": round(x_ms, 3)}
 
 
+def profile_figures(N, L, batch, alg_bytes, world):
+    """Roofline fields from the committed single-GPU profiles of the default command (rocprofv3 kernel trace via
+    tools/prof_agree.py, FETCH_SIZE / WRITE_SIZE passes via tools/pmc_summary.py).  At N = 1 they are this
+    command's own figures and go into `roofline` directly; at N > 1 they describe another run, so they are
+    returned only under `profile_1gpu`, labelled (tests/test_bench_cli.py checks both forms)."""
+    prof = {}
+    tr = pmc_traffic(N, L, batch)
+    if tr:
+        prof["traffic"] = tr[0]
+        prof["traffic_source"] = f"profiles/{tr[1]}"
+        prof["traffic_over_algorithmic"] = round(tr[0] / alg_bytes, 3)
+    tr = prof_trace(N, L, batch)
+    if tr:
+        # per-kernel averages of a committed rocprofv3 --kernel-trace run of this same command: the roofline
+        # recomputed from the trace alone
+        prof["kernel_ms_per_transform"] = round(tr["rocprof_kernel_ms_per_transform"], 4)
+        prof["kernel_trace_frac"] = round(
+            alg_bytes / (tr["rocprof_kernel_ms_per_transform"] * 1e-3) / 1e9 / HBM_PEAK_GBS, 4)
+        prof["kernel_trace_source"] = f"profiles/{tr['file']}"
+        prof["kernel_trace_per_kernel_avg_us"] = {
+            k.split("(")[0].split("<")[0].replace("void mfhe::", ""): round(v["avg_us"], 2)
+            for k, v in tr["per_kernel"].items()}
+    if world == 1 or not prof:
+        return prof
+    prof["note"] = ("from the committed single-GPU profiles of the N = 1 command, not measured in this "
+                    f"{world}-rank run (per-GPU work is the same: weak scaling)")
+    return {"profile_1gpu": prof}
+
+
 def c4_line(world, rank, comm, barrier, reps=5):
     """BASELINE C4: encode -> encrypt_pair -> decrypt_and_decode with wide CRT at the reference geometry (n = 64,
     512 W-lanes), L = 16 moduli q = 1 mod 2^8 * 771, residues sharded across the ranks: rank g runs every
@@ -481,6 +510,15 @@ def c5_line(world, rank, barrier, timed, backend, reps=2, recv_gib=2.0):
             res[m]["path"] = ("mfhe_crt_recombine_chunked: RCCL exchange of chunk k+1 on the communicator's stream "
                               "beside the compose of chunk k, two receive halves" +
                               (" (1-rank communicator: the exchange is a device copy)" if world == 1 else ""))
+            # the same chunked call with the composes skipped (MFHE_RECOMBINE_EXCHANGE_ONLY): the exchange alone,
+            # so recombine_ms against exchange_only_ms + compose_ms shows how much of the two overlaps
+            w_x, _ = timed(lambda m=m: ctx_all.crt_recombine_chunked(comm, m, shard, batch, N, chunks[m], None,
+                                                                     stream=stream, flags=mfhe.RECOMBINE_EXCHANGE_ONLY),
+                           reps, 1)
+            res[m]["exchange_only_ms"] = round(w_x / reps * 1e3, 3)
+            if "local" in res:
+                # the local compose of all 4096 polys at N = 1 (its recombine_ms); a rank composes 1/G of them
+                res[m]["compose_only_ms_est"] = round(res["local"]["recombine_ms"] / world, 3)
     if comm is not None:
         comm.close()
     ctx.close()
@@ -642,18 +680,24 @@ def u64_line(reps=10):
     return res
 
 
+WATCHDOG_EXIT = 3   # exit status of a run whose secondary lines the watchdog stopped (the headline is printed)
+
+
 def start_watchdog(out: dict, rank: int, seconds: float):
     """After `seconds`, rank 0 prints `out` (the finished headline plus whatever secondary lines completed) with a
-    note, and every rank exits 0 without waiting for the GPU work or collectives in flight."""
+    note, and every rank exits WATCHDOG_EXIT without waiting for the GPU work or collectives in flight: a hang in a
+    multi-rank line fails the run visibly (non-zero status, passed through by launch_ranks) while the headline
+    measured before it is still on stdout."""
     import threading
 
     def bail():
         if rank == 0:
-            out["secondary_lines"] = f"stopped by the {seconds:.0f} s watchdog; lines finished before it are included"
+            out["secondary_lines"] = (f"stopped by the {seconds:.0f} s watchdog (exit status {WATCHDOG_EXIT}); "
+                                      f"lines finished before it are included")
             print(json.dumps(out), flush=True)
-        sys.stderr.write(f"bench.py rank {rank}: secondary lines exceeded {seconds} s, exiting\n")
+        sys.stderr.write(f"bench.py rank {rank}: secondary lines exceeded {seconds} s, exiting {WATCHDOG_EXIT}\n")
         sys.stderr.flush()
-        os._exit(0)
+        os._exit(WATCHDOG_EXIT)
     wd = threading.Timer(seconds, bail)
     wd.daemon = True
     wd.start()
@@ -693,6 +737,9 @@ def launch_ranks(n: int) -> int:
     rc = p.wait()
     if line is not None:
         print(line, flush=True)
+        # torch.distributed.run reports any failed rank as 1: restore the watchdog's own status
+        if rc != 0 and "watchdog" in str(json.loads(line).get("secondary_lines", "")):
+            return WATCHDOG_EXIT
     if rc == 0 and line is None:
         print("bench.py: the ranks exited 0 but printed no JSON line", file=sys.stderr)
         return 1
@@ -856,24 +903,9 @@ def main():
                                "algorithmic_bytes_per_launch": alg_bytes,
                                "hbm_read_frac": round(ach / 2 / HBM_PEAK_GBS, 4),
                                "event_ms_per_transform": round(res["fwd_ev_ms"], 4)}
-            tr = pmc_traffic(N, L, batch)
-            if tr:
-                out["roofline"]["traffic"] = tr[0]
-                out["roofline"]["traffic_source"] = f"profiles/{tr[1]}"
-                out["roofline"]["traffic_over_algorithmic"] = round(tr[0] / alg_bytes, 3)
+            out["roofline"].update(profile_figures(N, L, batch, alg_bytes, world))
             out["inverse_NTT_per_s"] = ntts / (res["inv_wall"] / args.steps)
             out["inverse_over_forward"] = round(out["inverse_NTT_per_s"] / out["value"], 4)
-            tr = prof_trace(N, L, batch)
-            if tr:
-                # per-kernel averages of a committed rocprofv3 --kernel-trace run of this same command
-                # (tools/prof_agree.py): the roofline recomputed from the trace alone
-                out["roofline"]["kernel_ms_per_transform"] = round(tr["rocprof_kernel_ms_per_transform"], 4)
-                out["roofline"]["kernel_trace_frac"] = round(
-                    alg_bytes / (tr["rocprof_kernel_ms_per_transform"] * 1e-3) / 1e9 / HBM_PEAK_GBS, 4)
-                out["roofline"]["kernel_trace_source"] = f"profiles/{tr['file']}"
-                out["roofline"]["kernel_trace_per_kernel_avg_us"] = {
-                    k.split("(")[0].split("<")[0].replace("void mfhe::", ""): round(v["avg_us"], 2)
-                    for k, v in tr["per_kernel"].items()}
         if "crt_ev_ms" in res:
             cb = res["crt_batch"]
             out["encode_crt_ops_per_s"] = cb / (res["crt_ev_ms"] * 1e-3) * world

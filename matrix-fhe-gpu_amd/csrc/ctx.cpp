@@ -725,6 +725,9 @@ extern "C" int mfhe_ctx_get_option(const mfhe_ctx* c, int opt, int64_t* v) {
     switch (opt) {
         case MFHE_OPT_NTT_CHUNK_BYTES: *v = c->ntt_chunk_bytes; return MFHE_OK;
         case MFHE_OPT_NTT_PLAN: *v = c->ntt_plan; return MFHE_OK;
+        case MFHE_OPT_NTT_PLAN_EFFECTIVE:
+            *v = mfhe::ntt_phantom_plan(c->arith == MFHE_ARITH_F64, c->logN, c->ntt_plan, true);
+            return MFHE_OK;
         case MFHE_OPT_NTT_WG_PER_CU: *v = c->ntt_wg_per_cu; return MFHE_OK;
         case MFHE_OPT_NTT_PREFETCH: *v = c->ntt_prefetch; return MFHE_OK;
         case MFHE_OPT_NTT_FUSED: *v = 0; return MFHE_OK;

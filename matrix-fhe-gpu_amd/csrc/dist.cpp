@@ -325,6 +325,12 @@ extern "C" int mfhe_crt_recombine_chunked_reserve(mfhe_ctx* ctx, mfhe_comm* c, i
     const size_t cp = chunk_polys_of(chunk_polys, (size_t)-1, c->nranks);
     size_t words = 0;
     if (int rc = xchg_shape(ctx, c, mode, cp, ncoeff, &words)) return rc;
+    // host-synchronising: the previous calls' composes are done, so the next call waits on no event of theirs
+    for (int b = 0; b < 2; ++b)
+        if (c->c_recorded[b]) {
+            MFHE_HIP(hipEventSynchronize(c->ev_c[b]));
+            c->c_recorded[b] = false;
+        }
     return grow(c, 2 * words * sizeof(uint64_t));
 }
 
@@ -337,30 +343,52 @@ extern "C" int mfhe_crt_recombine_chunked_reserve(mfhe_ctx* ctx, mfhe_comm* c, i
 // k * cp / G + j, the order of mfhe/dist.py owned_polys) or, with MFHE_RECOMBINE_ROWS_GLOBAL, the global
 // polynomial index p0 + rank * cp / G + j (rows of other ranks untouched).  Every chunk's exchange is complete
 // before s proceeds past this call (the last compose waits for the last exchange, and xs runs them in order).
+//
+// Collective safety.  Every check that can fail runs before the first exchange, on arguments every rank passes
+// alike.  Once the first exchange is issued, a local failure (a compose launch, an event call, the injected
+// MFHE_RECOMBINE_DEBUG_FAIL) does not return early: the remaining exchanges are still issued (their composes
+// skipped), so no peer is left inside a collective this rank never joins, and the first error is returned at the
+// end (with MFHE_RECOMBINE_AGREE every rank then also learns it through comm_agree).
 extern "C" int mfhe_crt_recombine_chunked(mfhe_ctx* ctx, mfhe_comm* c, int mode, const uint64_t* d_shard,
                                           size_t npoly, size_t ncoeff, size_t chunk_polys, double* d_out,
                                           size_t out_stride, int flags, mfhe_stream_t s) {
     size_t words = 0;
     if (int rc = xchg_shape(ctx, c, mode, npoly, ncoeff, &words)) return rc;   // G | L, G | npoly, mode
     if (npoly == 0 || ncoeff == 0) return MFHE_OK;
-    if (!d_shard || !d_out || out_stride == 0) return set_error(MFHE_EINVAL, "recombine: bad pointer / stride");
-    if (flags & ~MFHE_RECOMBINE_ROWS_GLOBAL) return set_error(MFHE_EINVAL, "recombine: unknown flags");
+    constexpr int kKnown = MFHE_RECOMBINE_ROWS_GLOBAL | MFHE_RECOMBINE_EXCHANGE_ONLY | MFHE_RECOMBINE_AFTER_PREV |
+                           MFHE_RECOMBINE_AGREE | MFHE_RECOMBINE_DEBUG_FAIL;
+    if (!d_shard || (!d_out && !(flags & MFHE_RECOMBINE_EXCHANGE_ONLY)) || out_stride == 0)
+        return set_error(MFHE_EINVAL, "recombine: bad pointer / stride");
+    if (flags & ~kKnown) return set_error(MFHE_EINVAL, "recombine: unknown flags");
     if (int rc = need_rccl()) return rc;
     const int G = c->nranks;
     const size_t lg = (size_t)(ctx->L / G), cp = chunk_polys_of(chunk_polys, npoly, G);
     size_t cw = 0;
     if (int rc = xchg_shape(ctx, c, mode, cp, ncoeff, &cw)) return rc;
-    if (int rc = grow(c, 2 * cw * sizeof(uint64_t))) return rc;
+    if (int rc = grow(c, 2 * cw * sizeof(uint64_t))) return rc;   // no-op after mfhe_crt_recombine_chunked_reserve
     uint64_t* half[2] = {static_cast<uint64_t*>(c->recv), static_cast<uint64_t*>(c->recv) + cw};
     const hipStream_t st = (hipStream_t)s;
-    MFHE_HIP(hipEventRecord(c->ev_in, st));
-    MFHE_HIP(hipStreamWaitEvent(c->xs, c->ev_in, 0));
+    int err = MFHE_OK;   // first local failure after the exchanges started; later composes are skipped
+    std::string err_msg;
+    auto fail = [&](int rc) {
+        if (rc && !err) {
+            err = rc;
+            err_msg = mfhe_last_error();
+        }
+    };
+    auto hip = [&](hipError_t he, const char* what) {
+        if (he != hipSuccess) fail(mfhe::hip_error(he, what));
+    };
+    if (!(flags & MFHE_RECOMBINE_AFTER_PREV)) {
+        hip(hipEventRecord(c->ev_in, st), "hipEventRecord");
+        hip(hipStreamWaitEvent(c->xs, c->ev_in, 0), "hipStreamWaitEvent");
+    }
     size_t k = 0;
     for (size_t p0 = 0; p0 < npoly; p0 += cp, ++k) {
         const size_t n = npoly - p0 < cp ? npoly - p0 : cp;   // polys of this chunk (a multiple of G)
         const size_t bs = n / (size_t)G, shard = n * lg * ncoeff;
         const int b = (int)(k & 1);
-        if (c->c_recorded[b]) MFHE_HIP(hipStreamWaitEvent(c->xs, c->ev_c[b], 0));
+        if (c->c_recorded[b]) hip(hipStreamWaitEvent(c->xs, c->ev_c[b], 0), "hipStreamWaitEvent");
         const uint64_t* send = d_shard + p0 * lg * ncoeff;
         ncclResult_t e;
         size_t off, stride;
@@ -373,15 +401,21 @@ extern "C" int mfhe_crt_recombine_chunked(mfhe_ctx* ctx, mfhe_comm* c, int mode,
             off = 0;
             stride = bs * lg * ncoeff;
         }
+        // an RCCL error leaves the communicator unusable (RCCL's own contract): nothing to keep in step with
         if (e != ncclSuccess) return nccl_error(e, mode == MFHE_XCHG_ALLGATHER ? "ncclAllGather" : "ncclAllToAll");
-        MFHE_HIP(hipEventRecord(c->ev_x[b], c->xs));
-        MFHE_HIP(hipStreamWaitEvent(st, c->ev_x[b], 0));
-        const size_t row = (flags & MFHE_RECOMBINE_ROWS_GLOBAL) ? p0 + (size_t)c->rank * bs : p0 / (size_t)G;
-        if (int rc = mfhe_crt_compose_f64_sharded(ctx, half[b] + off, G, stride, bs, ncoeff,
-                                                  d_out + row * ncoeff * out_stride, out_stride, s))
-            return rc;
-        MFHE_HIP(hipEventRecord(c->ev_c[b], st));
+        hip(hipEventRecord(c->ev_x[b], c->xs), "hipEventRecord");
+        hip(hipStreamWaitEvent(st, c->ev_x[b], 0), "hipStreamWaitEvent");
+        if ((flags & MFHE_RECOMBINE_DEBUG_FAIL) && k == (npoly > cp ? 1u : 0u))
+            fail(set_error(MFHE_EHIP, "recombine: injected compose failure (MFHE_RECOMBINE_DEBUG_FAIL)"));
+        if (!err && !(flags & MFHE_RECOMBINE_EXCHANGE_ONLY)) {
+            const size_t row = (flags & MFHE_RECOMBINE_ROWS_GLOBAL) ? p0 + (size_t)c->rank * bs : p0 / (size_t)G;
+            fail(mfhe_crt_compose_f64_sharded(ctx, half[b] + off, G, stride, bs, ncoeff,
+                                              d_out + row * ncoeff * out_stride, out_stride, s));
+        }
+        // recorded even when the compose was skipped: s has passed the exchange, so half b may be refilled
+        hip(hipEventRecord(c->ev_c[b], st), "hipEventRecord");
         c->c_recorded[b] = true;
     }
-    return MFHE_OK;
+    if (flags & MFHE_RECOMBINE_AGREE) return mfhe::comm_agree(c, err ? set_error(err, err_msg) : MFHE_OK, st);
+    return err ? set_error(err, err_msg) : MFHE_OK;
 }

@@ -815,8 +815,10 @@ static int decode_sharded_impl(mfhe_ctx* c, mfhe_ctx* call, mfhe_comm* comm, int
     uint64_t* coeff_im = pb->get<uint64_t>(g.words);
     double2* ccx = pb->get<double2>(g.cnt);
     double2* ecx = pb->get<double2>(g.cnt);
-    // both W-INTTs first, then the two chunked recombines back to back: the exchange stream runs the re and im
-    // chunks without a gap while this stream composes (dist.cpp mfhe_crt_recombine_chunked).  Rows land at their
+    // both W-INTTs first, then the two chunked recombines back to back; the im call passes MFHE_RECOMBINE_AFTER_PREV
+    // (coeff_im was complete when the re call was entered), so the exchange stream runs the im chunks right after the
+    // re chunks, waiting only for the composes whose receive half it refills (dist.cpp mfhe_crt_recombine_chunked).
+    // Rows land at their
     // lane index (MFHE_RECOMBINE_ROWS_GLOBAL), so each chunk's lanes [p0, p0 + cp) are [rank][cp / G] in lane order
     // and one in-place all-gather per chunk completes them on every rank.
     const size_t cp = mfhe_ctx::PHI / 4 >= (size_t)G ? mfhe_ctx::PHI / 4 / G * G : (size_t)G;
@@ -825,7 +827,7 @@ static int decode_sharded_impl(mfhe_ctx* c, mfhe_ctx* call, mfhe_comm* comm, int
     RC(mfhe_crt_recombine_chunked(call, comm, mode, coeff_re, 512, g.n2, cp, (double*)ccx, 2,
                                   MFHE_RECOMBINE_ROWS_GLOBAL, (mfhe_stream_t)s));
     RC(mfhe_crt_recombine_chunked(call, comm, mode, coeff_im, 512, g.n2, cp, (double*)ccx + 1, 2,
-                                  MFHE_RECOMBINE_ROWS_GLOBAL, (mfhe_stream_t)s));
+                                  MFHE_RECOMBINE_ROWS_GLOBAL | MFHE_RECOMBINE_AFTER_PREV, (mfhe_stream_t)s));
     for (size_t p0 = 0; p0 < 512; p0 += cp) {
         const size_t bs = (512 - p0 < cp ? 512 - p0 : cp) / (size_t)G;
         RC(comm_allgather_bytes(comm, ccx + (p0 + (size_t)rank * bs) * g.n2, ccx + p0 * g.n2,

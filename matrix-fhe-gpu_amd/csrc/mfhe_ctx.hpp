@@ -66,6 +66,18 @@ struct NttTablesU {   // U64 path / phantom format
 
 }  // namespace mfhe
 
+namespace mfhe {
+// The launch plan a phantom NTT call runs (MFHE_OPT_NTT_PLAN_EFFECTIVE; ntt_plans.hpp run_phantom follows it):
+// 4 = the pipelined single pass (N = 2^14, FP64, context limb table), 1 = one pass per polynomial (plain), 2 = two
+// passes.  plan: MFHE_OPT_NTT_PLAN (0 / 3 auto, 1 single, 2 two passes from log_n 12).
+inline int ntt_phantom_plan(bool f64, int logN, int plan, bool limbs) {
+    const bool autoplan = plan == 0 || plan == 3;
+    if (f64 && logN == 14 && limbs && autoplan) return 4;
+    const bool two = logN > 14 || (plan == 2 && logN >= 12) || (autoplan && logN == 14);
+    return two ? 2 : 1;
+}
+}  // namespace mfhe
+
 struct mfhe_ctx {
     int L = 0;
     int logN = 0;

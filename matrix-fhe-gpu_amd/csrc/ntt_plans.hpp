@@ -302,14 +302,16 @@ static int two_pass(const NttJob<TS>& j, hipStream_t st) {
 
 template <class A, class TS, bool INV>
 static int run_phantom(const NttJob<TS>& j, hipStream_t st) {
-    // auto: N = 2^14 runs two passes (7 + 7, 8-row block tiles): at C2 +1% forward, +7% inverse over the single
-    // pass, which holds one 2^14 polynomial per CU (139 KiB of LDS) and cannot overlap loads with butterflies
-    // (profiles/r02_c2_plans2.txt)
+    // auto (plan 0, or 3): N = 2^14 with FP64 arithmetic and the context's limb table runs the pipelined single pass
+    // (ntt_single14.hpp, one polynomial per CU with the next one's loads in flight, 16N bytes); otherwise (U64, or
+    // the raw phantom entry points without a limb table) two passes (7 + 7): the plain single pass holds one 2^14
+    // polynomial per CU and cannot overlap loads with butterflies (profiles/r02_c2_plans2.txt).  Plan 1 / 2 keep
+    // the plain single pass / two passes for A/B.
+    const int kind = ntt_phantom_plan(std::is_same<A, ArithF64>::value, j.logN, j.plan, j.limbs != nullptr);
     if constexpr (std::is_same<A, ArithF64>::value) {
-        // N = 2^14: the pipelined single pass (plan 0 = auto, or 3); plan 1 / 2 keep the earlier plans for A/B
-        if (j.logN == 14 && j.limbs && (j.plan == 0 || j.plan == 3)) return launch_s14<INV>(j, st);
+        if (kind == 4) return launch_s14<INV>(j, st);
     }
-    const bool two = j.logN > 14 || (j.plan == 2 && j.logN >= 12) || (j.plan == 0 && j.logN == 14);
+    const bool two = kind == 2;
     if (!two) return run_single<A, TS, INV, false>(j, st);
     switch (j.logN) {
         case 12: return two_pass<A, TS, 6, 64, 6, 64, INV>(j, st);

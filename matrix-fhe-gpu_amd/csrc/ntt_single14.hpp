@@ -24,7 +24,8 @@
 //   L3: k -> b3..b0, lane bits 0..3 -> b8..b5, lane bit 4 -> b4, lane bit 5 -> b9, wave -> b13..b10
 // Forward (CT, stage s pairs bit 13 - s): load L0, stages 0-3 | L1 4-7 | L2 8-10 (b2 rides along) | L3 11-13 | -> L1,
 // store.  Inverse (GS): load L1 -> L3 stages 13-11 | L2 10-8 | L1 7-4 | L0 3-0 (n^-1 at s = 0), store.  Only L0 is
-// cross-wave: two workgroup barriers per polynomial (r04), the other exchanges are wave-local.
+// cross-wave: one workgroup barrier per polynomial (after the cross-wave image is written; the wait before the
+// polynomial's first LDS write is the drain counter, see below), the other exchanges are wave-local.
 // Arithmetic and reduction schedule as in NttPass (ntt_arith.hpp): forward, one centred reduction at the start of
 // every round after the first (rounds of <= 4 stages: |x| < 3q); inverse, lazy GS on every other stage.
 // Reference: phantom fnwt_1d / inwt_1d per polynomial (ntt_core.cu:443-460); same outputs, bit for bit.

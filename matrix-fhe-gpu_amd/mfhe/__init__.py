@@ -28,8 +28,13 @@ OPT_NTT_FUSED, OPT_WCRT_MFMA = 6, 9   # OPT_NTT_FUSED: removed in r04, only 0 ac
 OPT_CGEMM_MFMA, OPT_HE_FUSED, OPT_TRACE_SPLIT = 10, 11, 12
 XCHG_ALLGATHER, XCHG_ALLTOALL = 0, 1
 RECOMBINE_ROWS_GLOBAL = 1
+RECOMBINE_EXCHANGE_ONLY = 2     # measurement: exchanges only, composes skipped (out untouched)
+RECOMBINE_AFTER_PREV = 4        # the shard was complete when the previous chunked call on the comm was entered
+RECOMBINE_AGREE = 8             # end with an all-rank status agreement (host wait)
+RECOMBINE_DEBUG_FAIL = 256      # test hook: the compose of chunk 1 (or 0) fails
 OPT_NTT_PACK = 13
 OPT_WCRT_PIPE = 14
+OPT_NTT_PLAN_EFFECTIVE = 15   # read-only: 4 pipelined single pass (2^14 FP64), 1 single pass, 2 two passes
 COMM_ID_BYTES = 128
 
 #: reference parameters (include/core/config.h:7-52)
@@ -407,18 +412,21 @@ class Context:
         check(lib.mfhe_crt_recombine_reserve(self._h, comm._h, m, npoly, ncoeff), "crt_recombine_reserve")
 
     def crt_recombine_chunked(self, comm: "Comm", mode, shard, npoly, ncoeff, chunk_polys, out, out_stride=1,
-                              rows_global=False, stream=None):
+                              rows_global=False, stream=None, flags=0):
         """Chunked, pipelined RCCL recombine (include/mfhe.h mfhe_crt_recombine_chunked): exchange of chunk k + 1
         on the communicator's stream beside the compose of chunk k on `stream`.  out rows: owned_polys order
-        (npoly/G rows), or the global poly index with rows_global (npoly rows, only this rank's written)."""
+        (npoly/G rows), or the global poly index with rows_global (npoly rows, only this rank's written).
+        flags: further MFHE_RECOMBINE_* bits (RECOMBINE_EXCHANGE_ONLY: out may be None)."""
         m = _XCHG[mode] if isinstance(mode, str) else mode
         g = comm.size
         lg = self.info().num_limbs // g if g else 0
         _need(shard, npoly * lg * ncoeff, "shard")
         rows = npoly if rows_global else (npoly // g if g else 0)
-        _need_strided(out, rows * ncoeff, out_stride, "out")
-        check(lib.mfhe_crt_recombine_chunked(self._h, comm._h, m, _ptr(shard), npoly, ncoeff, chunk_polys, _ptr(out),
-                                             out_stride, RECOMBINE_ROWS_GLOBAL if rows_global else 0,
+        if out is not None or not flags & RECOMBINE_EXCHANGE_ONLY:
+            _need_strided(out, rows * ncoeff, out_stride, "out")
+        check(lib.mfhe_crt_recombine_chunked(self._h, comm._h, m, _ptr(shard), npoly, ncoeff, chunk_polys,
+                                             _ptr(out) if out is not None else None, out_stride,
+                                             (RECOMBINE_ROWS_GLOBAL if rows_global else 0) | flags,
                                              _stream_ptr(stream)), "crt_recombine_chunked")
         return out
 

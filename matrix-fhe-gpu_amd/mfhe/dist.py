@@ -81,7 +81,8 @@ def owned_polys(batch: int, world: int, rank: int, chunk_polys: int) -> list[int
 
 
 def crt_recombine_chunked(ctx, shard: torch.Tensor, batch: int, ncoeff: int, mode: str, chunk_polys: int,
-                          out: torch.Tensor, group=None, stream=None, comm=None, rows_global: bool = False) -> torch.Tensor:
+                          out: torch.Tensor, group=None, stream=None, comm=None, rows_global: bool = False,
+                          flags: int = 0) -> torch.Tensor:
     """crt_recombine over chunk_plan's poly chunks: shard [batch][Lg][ncoeff] -> out f64, rows in owned_polys
     order ([batch/world][ncoeff]) or, with rows_global, at the global poly index ([batch][ncoeff], only this
     rank's rows written).  Each chunk is one exchange + in-place sharded compose.  With `comm` the whole loop is
@@ -90,7 +91,9 @@ def crt_recombine_chunked(ctx, shard: torch.Tensor, batch: int, ncoeff: int, mod
     which the gloo tests use to pin the same row order."""
     if comm is not None:
         return ctx.crt_recombine_chunked(comm, mode, shard, batch, ncoeff, chunk_polys, out, stream=stream,
-                                         rows_global=rows_global)
+                                         rows_global=rows_global, flags=flags)
+    if flags:
+        raise ValueError("crt_recombine_chunked: flags need the native path (comm)")
     world = dist.get_world_size(group)
     rank = dist.get_rank(group)
     lg = ctx.info().num_limbs // world

@@ -44,8 +44,33 @@ def test_world_size_mismatch_fails_loudly():
 
 
 def test_watchdog_prints_the_headline_when_a_secondary_line_hangs():
-    """Both ranks stall in a 'secondary line' for 60 s; the 3 s watchdog prints rank 0's line and every rank exits 0."""
+    """Both ranks stall in a 'secondary line' for 60 s; the 3 s watchdog prints rank 0's line and every rank exits
+    with the watchdog status (a hang in a multi-rank line must fail the run visibly, not exit 0), which
+    the self-launching parent passes through."""
+    import importlib.util
+    spec = importlib.util.spec_from_file_location("bench_mod", ROOT / "bench.py")
+    bench = importlib.util.module_from_spec(spec)
+    spec.loader.exec_module(bench)
     p = _run(["--gpus", "2", "--launch-check", "--hang-check", "60", "--secondary-timeout", "3"], timeout=50)
-    assert p.returncode == 0, p.stderr[-3000:]
+    assert p.returncode == bench.WATCHDOG_EXIT != 0, p.stderr[-3000:]
     (line,) = _json_lines(p.stdout)
     assert line["n_gpus"] == 2 and "watchdog" in line["secondary_lines"]
+
+
+def test_multi_rank_line_carries_no_unlabelled_one_gpu_profile_figures():
+    """the committed rocprofv3 / PMC figures are this command's own only at N = 1; at N > 1 the
+    roofline must not carry them as if measured (kernel_trace_*, traffic) -- they sit under profile_1gpu, with a
+    note."""
+    import importlib.util
+    spec = importlib.util.spec_from_file_location("bench_mod", ROOT / "bench.py")
+    bench = importlib.util.module_from_spec(spec)
+    spec.loader.exec_module(bench)
+    N, L, B = 1 << 16, 8, 1024
+    alg = 16.0 * N * L * B
+    one = bench.profile_figures(N, L, B, alg, 1)
+    assert "traffic" in one and "kernel_trace_frac" in one   # the committed profiles of the default command
+    for world in (2, 4, 8):
+        many = bench.profile_figures(N, L, B, alg, world)
+        assert set(many) == {"profile_1gpu"}
+        assert not any(k.startswith("kernel_trace") or k.startswith("traffic") for k in many)
+        assert "not measured in this" in many["profile_1gpu"]["note"]

@@ -140,9 +140,79 @@ def test_chunked_recombine_rejects_bad_arguments(mfhe, orc):
             ctx.crt_recombine_chunked(comm, 7, d, 4, 16, 2, out)
         with pytest.raises(mfhe.MfheError):   # unknown flag bits
             mfhe.check(mfhe.lib.mfhe_crt_recombine_chunked(ctx.handle, comm._h, 0, d.data_ptr(), 4, 16, 2,
-                                                           out.data_ptr(), 1, 6, None))
+                                                           out.data_ptr(), 1, 16, None))
         with pytest.raises(ValueError):   # undersized output caught on the host
             ctx.crt_recombine_chunked(comm, "alltoall", d, 4, 16, 2, out[:10])
+    finally:
+        comm.close()
+        ctx.close()
+
+
+@pytest.mark.parametrize("agree", [False, True])
+def test_chunked_recombine_injected_failure_keeps_communicator_usable(mfhe, orc, agree):
+    """a local failure after the exchanges started (MFHE_RECOMBINE_DEBUG_FAIL fails the compose of
+    chunk 1) returns an error once every remaining exchange was still issued -- no return in the middle of the
+    chunk loop -- and the communicator stays usable: the next call on it is bit-exact.  With
+    MFHE_RECOMBINE_AGREE the error also goes through the all-rank status agreement."""
+    import torch
+    moduli = orc.gen_primes(50, 1 << 18, 8)
+    ctx = mfhe.Context(moduli, 16)
+    npoly, ncoeff = 11, 1 << 12
+    rng = np.random.default_rng(7)
+    res, _ = _residues(rng, npoly, moduli, ncoeff, ctx.info().delta)
+    d = mfhe.to_device_u64(res.ravel())
+    ref = torch.empty(npoly * ncoeff, dtype=torch.float64, device="cuda")
+    ctx.crt_compose_f64(d, ref, npoly, ncoeff)
+    comm = mfhe.Comm.from_id(mfhe.Comm.unique_id(), 1, 0)
+    try:
+        ctx.crt_recombine_chunked_reserve(comm, "alltoall", 4, ncoeff)
+        out = torch.full((npoly * ncoeff,), float("nan"), dtype=torch.float64, device="cuda")
+        flags = mfhe.RECOMBINE_DEBUG_FAIL | (mfhe.RECOMBINE_AGREE if agree else 0)
+        with pytest.raises(mfhe.MfheError, match="injected"):
+            ctx.crt_recombine_chunked(comm, "alltoall", d, npoly, ncoeff, 4, out, flags=flags)
+        torch.cuda.synchronize()
+        o = out.view(npoly, ncoeff)
+        assert torch.equal(o[:4], ref.view(npoly, ncoeff)[:4])   # chunk 0 composed before the failure
+        assert torch.isnan(o[4:]).all()                          # chunks 1, 2: exchanged, not composed
+        for _ in range(2):   # the communicator and its receive halves are usable afterwards
+            out.fill_(float("nan"))
+            ctx.crt_recombine_chunked(comm, "alltoall", d, npoly, ncoeff, 4, out)
+            torch.cuda.synchronize()
+            assert torch.equal(out, ref)
+    finally:
+        comm.close()
+        ctx.close()
+
+
+def test_chunked_recombine_exchange_only_and_after_prev(mfhe, orc):
+    """MFHE_RECOMBINE_EXCHANGE_ONLY (bench.py's exchange_only_ms) leaves the output untouched and accepts a null
+    one; MFHE_RECOMBINE_AFTER_PREV (the decode's im call right after its re call) gives the same result as a
+    plain call when the shard was ready at the previous call."""
+    import torch
+    moduli = orc.gen_primes(50, 1 << 18, 8)
+    ctx = mfhe.Context(moduli, 16)
+    npoly, ncoeff = 9, 1 << 12
+    rng = np.random.default_rng(9)
+    res, _ = _residues(rng, npoly, moduli, ncoeff, ctx.info().delta)
+    d = mfhe.to_device_u64(res.ravel())
+    d2 = mfhe.to_device_u64(res[::-1].copy().ravel())
+    ref = torch.empty(npoly * ncoeff, dtype=torch.float64, device="cuda")
+    ref2 = torch.empty_like(ref)
+    ctx.crt_compose_f64(d, ref, npoly, ncoeff)
+    ctx.crt_compose_f64(d2, ref2, npoly, ncoeff)
+    comm = mfhe.Comm.from_id(mfhe.Comm.unique_id(), 1, 0)
+    try:
+        ctx.crt_recombine_chunked_reserve(comm, "allgather", 2, ncoeff)
+        out = torch.full((npoly * ncoeff,), float("nan"), dtype=torch.float64, device="cuda")
+        ctx.crt_recombine_chunked(comm, "allgather", d, npoly, ncoeff, 2, out, flags=mfhe.RECOMBINE_EXCHANGE_ONLY)
+        ctx.crt_recombine_chunked(comm, "allgather", d, npoly, ncoeff, 2, None, flags=mfhe.RECOMBINE_EXCHANGE_ONLY)
+        torch.cuda.synchronize()
+        assert torch.isnan(out).all()
+        out2 = torch.full_like(out, float("nan"))
+        ctx.crt_recombine_chunked(comm, "allgather", d, npoly, ncoeff, 2, out)
+        ctx.crt_recombine_chunked(comm, "allgather", d2, npoly, ncoeff, 2, out2, flags=mfhe.RECOMBINE_AFTER_PREV)
+        torch.cuda.synchronize()
+        assert torch.equal(out, ref) and torch.equal(out2, ref2)
     finally:
         comm.close()
         ctx.close()

@@ -323,6 +323,27 @@ def test_single_pass_14_matches_oracle_and_other_plans(mfhe, orc, batch, nl, sta
         np.testing.assert_array_equal(mfhe.to_host_u64(d), orc.phantom_inv(data, nl, log_n, sub))
 
 
+def test_plan_3_is_auto_for_u64_at_14(mfhe, orc):
+    """MFHE_OPT_NTT_PLAN 3 is documented as auto (include/mfhe.h): on the U64 path at log_n 14 it must run auto's two
+    passes, not fall through to the plain single pass (ADVICE r04).  Checked by output (oracle) under plans 0 and 3
+    and by the plan the context reports (OPT_NTT_PLAN_EFFECTIVE, the function the planner itself uses)."""
+    import torch
+    log_n, N = 14, 1 << 14
+    moduli = orc.gen_primes(60, 4 * N, 2)
+    ctx = mfhe.Context(moduli, log_n)
+    assert ctx.info().arith == mfhe.ARITH_U64   # 60-bit primes: the FP64 path cannot take them
+    data = rand_residues(np.random.default_rng(14), 3, moduli, N)
+    want = orc.phantom_fwd(data, 2, log_n, moduli)
+    for plan in (0, 3):
+        ctx.set_option(mfhe.OPT_NTT_PLAN, plan)
+        d = mfhe.to_device_u64(data)
+        ctx.ntt_fwd(d, batch=3)
+        torch.cuda.synchronize()
+        np.testing.assert_array_equal(mfhe.to_host_u64(d), want)
+        assert ctx.get_option(mfhe.OPT_NTT_PLAN_EFFECTIVE) == 2   # two passes
+    ctx.close()
+
+
 def test_fused_option_removed(mfhe, orc):
     """MFHE_OPT_NTT_FUSED (the one-launch XCD-L2 hand-off, r02-r03) was removed in r04: its hand-off was never
     proven (VERDICT r03 weak #6) and it was slower.  0 is still accepted; anything else fails loudly."""
