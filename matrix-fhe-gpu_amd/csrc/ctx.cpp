@@ -606,6 +606,7 @@ extern "C" int mfhe_ctx_create(const uint64_t* moduli, int L, int log_n, int con
 extern "C" int mfhe_ctx_destroy(mfhe_ctx* c) {
     if (!c) return MFHE_OK;
     if (c->ws) (void)hipFree(c->ws);
+    if (c->d_xl2) (void)hipFree(c->d_xl2);
     if (c->gemm_ws) (void)hipFree(c->gemm_ws);
     if (c->wd_ws) (void)hipFree(c->wd_ws);
     for (void* p : c->allocs) (void)hipFree(p);
@@ -653,7 +654,7 @@ extern "C" int mfhe_ctx_set_option(mfhe_ctx* c, int opt, int64_t v) {
             c->ntt_chunk_bytes = v;
             return MFHE_OK;
         case MFHE_OPT_NTT_PLAN:
-            if (v < 0 || v > 3) return set_error(MFHE_EINVAL, "plan must be 0, 1, 2 or 3");
+            if (v < 0 || v > 5 || v == 4) return set_error(MFHE_EINVAL, "plan must be 0, 1, 2, 3 or 5");
             c->ntt_plan = (int)v;
             return MFHE_OK;
         case MFHE_OPT_NTT_WG_PER_CU:
@@ -725,6 +726,12 @@ extern "C" int mfhe_ctx_get_option(const mfhe_ctx* c, int opt, int64_t* v) {
     switch (opt) {
         case MFHE_OPT_NTT_CHUNK_BYTES: *v = c->ntt_chunk_bytes; return MFHE_OK;
         case MFHE_OPT_NTT_PLAN: *v = c->ntt_plan; return MFHE_OK;
+        case MFHE_OPT_NTT_XL2_TIMEOUT: {   // synchronous read of the plan-5 kernel's sticky timeout word (tests)
+            uint32_t w = 0;
+            if (c->d_xl2) MFHE_HIP(hipMemcpy(&w, c->d_xl2 + 513, sizeof w, hipMemcpyDeviceToHost));
+            *v = w;
+            return MFHE_OK;
+        }
         case MFHE_OPT_NTT_PLAN_EFFECTIVE:
             *v = mfhe::ntt_phantom_plan(c->arith == MFHE_ARITH_F64, c->logN, c->ntt_plan, true);
             return MFHE_OK;

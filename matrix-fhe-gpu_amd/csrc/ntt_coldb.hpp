@@ -77,7 +77,7 @@ __device__ __forceinline__ void lds_barrier() { asm volatile("s_waitcnt lgkmcnt(
 // then the raw intermediate (F64: centred doubles; U64: [0, 2q)) stored to base (plain stores, R per thread).
 // tw0: tw[1..15] of the limb (shared), tw1: this thread's round-1 twiddles ((16 + tau) << e) + j.  TW0 / TW1:
 // anything indexable by [0, 15) giving A::Tw -- register arrays (F64), LDS table views (U64).
-template <class A, class TW0, class TW1, class HOOK>
+template <class A, bool STORE = true, class TW0, class TW1, class HOOK>
 __device__ __forceinline__ void coldb_tile(uint64_t* buf, uint32_t gl, uint32_t tau, const LimbConst& lc,
                                            const TW0& tw0, const TW1& tw1, uint64_t* base, uint32_t off0, int logS,
                                            HOOK&& after_reads) {
@@ -115,8 +115,11 @@ __device__ __forceinline__ void coldb_tile(uint64_t* buf, uint32_t gl, uint32_t 
     });
     // intermediate, the same words NttPass<COLS, OUT_RAW> writes
 #pragma unroll
-    for (int k = 0; k < C::R; ++k)
-        base[off0 | ((uint32_t)Gm::g_of(1, tau, k) << logS)] = A::to_raw(ar.reduce(x[k]));
+    for (int k = 0; k < C::R; ++k) {
+        const uint64_t o = A::to_raw(ar.reduce(x[k]));
+        if constexpr (STORE) base[off0 | ((uint32_t)Gm::g_of(1, tau, k) << logS)] = o;
+        else asm volatile("" ::"v"(o));   // timing probe (ntt_xl2.hpp MFHE_XL2_PROBE): no store
+    }
 }
 
 // U64 twiddle views of a limb's table T = tw[0, 256) (value and Shoup companion) held in LDS

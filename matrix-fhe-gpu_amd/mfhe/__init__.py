@@ -34,7 +34,8 @@ RECOMBINE_AGREE = 8             # end with an all-rank status agreement (host wa
 RECOMBINE_DEBUG_FAIL = 256      # test hook: the compose of chunk 1 (or 0) fails
 OPT_NTT_PACK = 13
 OPT_WCRT_PIPE = 14
-OPT_NTT_PLAN_EFFECTIVE = 15   # read-only: 4 pipelined single pass (2^14 FP64), 1 single pass, 2 two passes
+OPT_NTT_PLAN_EFFECTIVE = 15   # read-only: 4 pipelined single pass (2^14 FP64), 1 single pass, 2 two passes, 5 XL2
+OPT_NTT_XL2_TIMEOUT = 16      # read-only: the plan-5 kernel's sticky timeout word (synchronous)
 COMM_ID_BYTES = 128
 
 #: reference parameters (include/core/config.h:7-52)
