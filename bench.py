@@ -673,6 +673,8 @@ def u64_line(reps=10):
             out[f"{kind}_alg_GBps"] = round(16.0 * N * r / 1e9, 1)
         out["frac_fwd"] = round(out["fwd_alg_GBps"] / HBM_PEAK_GBS, 4)
         out["arith"] = "u64" if ctx.info().arith == mfhe.ARITH_U64 else "f64"
+        if out["arith"] == "u64":   # forward schedule: lazy U60 (every q < 2^60) or Harvey
+            out["fwd_schedule"] = "u60" if ctx.get_option(mfhe.OPT_NTT_U60) else "harvey"
         out["max_modulus_bits"] = max(moduli).bit_length()
         res[name] = out
         del d

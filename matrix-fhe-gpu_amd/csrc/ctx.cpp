@@ -507,6 +507,7 @@ static int ctx_create_impl(const uint64_t* moduli, int L, int logN, int conv, do
     c->moduli.assign(moduli, moduli + L);
     c->f64_ok = std::all_of(c->moduli.begin(), c->moduli.end(), [](uint64_t q) { return q < (1ull << 50); });
     c->arith = c->f64_ok ? MFHE_ARITH_F64 : MFHE_ARITH_U64;
+    c->u60_ok = std::all_of(c->moduli.begin(), c->moduli.end(), [](uint64_t q) { return q < (1ull << 60); });
     hipError_t he = hipGetDevice(&c->device);
     int rc = MFHE_OK;
     if (he != hipSuccess) rc = hip_error(he, "hipGetDevice");
@@ -694,6 +695,10 @@ extern "C" int mfhe_ctx_set_option(mfhe_ctx* c, int opt, int64_t v) {
             if (v < 0 || v > 2) return set_error(MFHE_EINVAL, "trace split must be 0, 1 or 2");
             c->trace_split = (int)v;
             return MFHE_OK;
+        case MFHE_OPT_NTT_U60:
+            if (v < 0 || v > 1) return set_error(MFHE_EINVAL, "ntt u60 must be 0 or 1");
+            c->ntt_u60 = (int)v;
+            return MFHE_OK;
         case MFHE_OPT_CRT_WORDS:
             if (v < 1 || v > 32) return set_error(MFHE_EINVAL, "crt words must be in [1, 32]");
             if (v <= c->W) return MFHE_OK;
@@ -745,6 +750,7 @@ extern "C" int mfhe_ctx_get_option(const mfhe_ctx* c, int opt, int64_t* v) {
         case MFHE_OPT_HE_FUSED: *v = c->he_fused; return MFHE_OK;
         case MFHE_OPT_TRACE_SPLIT: *v = c->trace_split; return MFHE_OK;
         case MFHE_OPT_CRT_WORDS: *v = c->W; return MFHE_OK;
+        case MFHE_OPT_NTT_U60: *v = c->ntt_u60 && c->u60_ok; return MFHE_OK;
         default: return set_error(MFHE_EINVAL, "unknown option");
     }
 }

@@ -14,11 +14,15 @@
 //    Used when any modulus is >= 2^50 and for the phantom fnwt_1d/inwt_1d surface,
 //    whose callers hand us u64 Shoup tables.
 //
-// Both produce canonical [0,q) outputs, so results are bit-identical to each
+//  * ArithU60 -- the same Shoup products with a lazier reduction schedule, for forward
+//    transforms of contexts whose moduli are all < 2^60 (below).
+//
+// All produce canonical [0,q) outputs, so results are bit-identical to each
 // other and to the phantom/reference transforms they restate.
 #pragma once
 #include <hip/hip_runtime.h>
 #include <cstdint>
+#include <type_traits>
 
 namespace mfhe {
 
@@ -90,6 +94,8 @@ struct ArithF64 {
     }
     // start-of-round reduction (keeps CT growth bounded)
     __device__ __forceinline__ double round_reduce(double x) const { return reduce(x); }
+    __device__ __forceinline__ void ct_first(double& u, double& v, Tw w) const { ct(u, v, w); }
+    __device__ __forceinline__ uint64_t raw_out(double x) const { return to_raw(reduce(x)); }
     // exact canonical u64 in [0, q)
     __device__ __forceinline__ uint64_t canon(double x) const {
         double r = reduce(x);          // |r| <= q/2 + eps
@@ -121,12 +127,14 @@ struct ArithU64 {
     // (v_bfi_b32 on a v_ashrrev mask, no compare).
     uint64_t q, two_q, nq, n2q;   // nq = -q, n2q = -2q (mod 2^64)
 
-    __device__ __forceinline__ explicit ArithU64(const LimbConst& c)
+    __device__ __forceinline__ explicit ArithU64(const LimbConst& c, bool pin = true)
         : q(c.q), two_q(2 * c.q), nq(0 - c.q), n2q(0 - 2 * c.q) {
         // held as values: otherwise x + n2q is re-derived from q as a v_mad_u64_u32 by -2 (a quarter-rate
         // multiply) in every butterfly
-        asm volatile("" : "+v"(nq));
-        asm volatile("" : "+v"(n2q));
+        if (pin) {
+            asm volatile("" : "+v"(nq));
+            asm volatile("" : "+v"(n2q));
+        }
     }
 
     __device__ __forceinline__ static uint64_t from_u64(uint64_t x) { return x; }
@@ -169,7 +177,77 @@ struct ArithU64 {
         x = sel_sub(x, x + n2q);
         return sel_sub(x, x + nq);
     }
+    // first CT stage of a round (executed-stage order) and the raw intermediate a pass writes: the Harvey policy
+    // reduces in every butterfly, so these are its ordinary ct / reduce
+    __device__ __forceinline__ void ct_first(uint64_t& u, uint64_t& v, Tw w) const { ct(u, v, w); }
+    __device__ __forceinline__ uint64_t raw_out(uint64_t x) const { return reduce(x); }
 };
+
+// ArithU60 -- forward transforms when every modulus of the context is < 2^60 (phantom's and SEAL's range):
+// 16q < 2^64 leaves room for a lazier schedule than Harvey's reduce-per-butterfly.
+//  * Values enter a round (an exchange-to-exchange run of <= 4 stages) below 16q.  Only the u inputs of the round's
+//    first stage are reduced, once, to [0, 8q) (one select by 8q); every CT adds at most 2q to the bound of its u
+//    input (u' = u + t, v' = u + 2q - t, t = Shoup product in [0, 2q) for any v < 2^64), so after 4 stages every
+//    value is below 8q + 8q = 16q again.  The v inputs never need a bound below 2^64.
+//  * A pass's raw intermediate is written unreduced (< 16q; the next pass's first stage reduces it) and the final
+//    canonicalisation is four selects (8q, 4q, 2q, q).
+//  * The Shoup product sums lo64(v w) and lo64(Q (-q)) in one mad chain: two v_mad_u64_u32 for the low halves, the
+//    four cross products into the high word by two v_add3.
+// VALU instructions per thread and tile: column pass 1753 -> 1449, block pass 1631 -> 1535 (profiles/r05_u64_isa.txt);
+// C3 60-bit forward 2.04 -> 2.22 M NTT/s in one rocprof run (profiles/r05_u60_kernel_stats.txt).  Constants are not
+// pinned to VGPRs here (ArithU64(c, false)): pinned, the column pass spilled at its 128-VGPR bound and fell back.
+struct ArithU60 : ArithU64 {
+    uint64_t n8q;
+    float qs;   // 2^32 / q (1 - 2^-20), canon's quotient scale
+
+    __device__ __forceinline__ explicit ArithU60(const LimbConst& c)
+        : ArithU64(c, false), n8q(0 - 8 * c.q), qs((float)(c.qinv * (4294967296.0 * (1.0 - 0x1p-20)))) {}
+    __device__ __forceinline__ uint64_t mulmod(uint64_t v, Tw w) const {
+        const uint64_t Q = mulhi64(v, w.y);
+        const uint32_t vl = (uint32_t)v, vh = (uint32_t)(v >> 32), wl = (uint32_t)w.x, wh = (uint32_t)(w.x >> 32);
+        const uint32_t Ql = (uint32_t)Q, Qh = (uint32_t)(Q >> 32), ml = (uint32_t)nq, mh = (uint32_t)(nq >> 32);
+        // the two low products spelled out: left to itself the compiler folds cross products into extra
+        // v_mad_u64_u32 + v_mov pairs
+        uint64_t p, p2, c1, c2;
+        asm("v_mad_u64_u32 %0, %1, %2, %3, 0" : "=v"(p), "=s"(c1) : "v"(vl), "v"(wl));
+        asm("v_mad_u64_u32 %0, %1, %2, %3, %4" : "=v"(p2), "=s"(c2) : "v"(Ql), "v"(ml), "v"(p));
+        const uint32_t hi = (uint32_t)(p2 >> 32) + vl * wh + vh * wl + Ql * mh + Qh * ml;
+        return ((uint64_t)hi << 32) | (uint32_t)p2;
+    }
+    __device__ __forceinline__ void ct(uint64_t& u, uint64_t& v, Tw w) const {
+        const uint64_t t = mulmod(v, w), a = u;
+        u = a + t;
+        v = a - t + two_q;
+    }
+    __device__ __forceinline__ void ct_first(uint64_t& u, uint64_t& v, Tw w) const {
+        u = sel_sub(u, u + n8q);
+        ct(u, v, w);
+    }
+    __device__ __forceinline__ uint64_t round_reduce(uint64_t x) const { return x; }
+    __device__ __forceinline__ uint64_t raw_out(uint64_t x) const { return x; }
+    // [0, 16q) -> [0, q): the quotient k = floor(x / q) - {0, 1} from the high word in FP32 (x / q < 16, so the
+    // high word's truncation and two FP32 roundings are far below 1; the scale is shaded down by 2^-20 so k never
+    // exceeds the quotient), x - k q in [0, 2q) by one mad, then one select: 10 VALU instructions instead of four
+    // selects' 20
+    __device__ __forceinline__ uint64_t canon(uint64_t x) const {
+        float f;
+        asm("v_cvt_f32_u32 %0, %1" : "=v"(f) : "v"((uint32_t)(x >> 32)));
+        uint32_t k;
+        asm("v_cvt_u32_f32 %0, %1" : "=v"(k) : "v"(f * qs));
+        uint64_t r, c;
+        asm("v_mad_u64_u32 %0, %1, %2, %3, %4" : "=v"(r), "=s"(c) : "v"(k), "v"((uint32_t)nq), "v"(x));
+        uint32_t kh;
+        asm("v_mul_lo_u32 %0, %1, %2" : "=v"(kh) : "v"(k), "v"((uint32_t)(nq >> 32)));
+        const uint32_t rh = (uint32_t)(r >> 32) + kh;
+        r = ((uint64_t)rh << 32) | (uint32_t)r;
+        return sel_sub(r, r + nq);
+    }
+};
+
+template <class A>
+constexpr bool kIsU64 = std::is_base_of<ArithU64, A>::value;   // the 64-bit integer policies (tables, LDS layouts)
+template <class A>
+constexpr bool kLazyU60 = std::is_same<A, ArithU60>::value;
 
 
 

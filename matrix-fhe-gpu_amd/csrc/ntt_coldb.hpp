@@ -110,13 +110,14 @@ __device__ __forceinline__ void coldb_tile(uint64_t* buf, uint32_t gl, uint32_t 
 #pragma unroll
         for (int k = 0; k < C::R; ++k) {
             if (k & half) continue;
-            ar.ct(x[k], x[k + half], tw1[(1 << e) - 1 + (k >> (bb + 1))]);
+            if constexpr (bb == 3) ar.ct_first(x[k], x[k + half], tw1[(1 << e) - 1 + (k >> (bb + 1))]);
+            else ar.ct(x[k], x[k + half], tw1[(1 << e) - 1 + (k >> (bb + 1))]);
         }
     });
     // intermediate, the same words NttPass<COLS, OUT_RAW> writes
 #pragma unroll
     for (int k = 0; k < C::R; ++k) {
-        const uint64_t o = A::to_raw(ar.reduce(x[k]));
+        const uint64_t o = ar.raw_out(x[k]);
         if constexpr (STORE) base[off0 | ((uint32_t)Gm::g_of(1, tau, k) << logS)] = o;
         else asm volatile("" ::"v"(o));   // timing probe (ntt_xl2.hpp MFHE_XL2_PROBE): no store
     }
@@ -237,7 +238,7 @@ __device__ __forceinline__ void coldb_twiddles(const double* tw, uint32_t tau, d
 template <class A, class TS, bool INV = false, bool SB = false>
 __global__ __launch_bounds__(ColDb::NT, SB ? MFHE_NTT_U64_COLDB_WAVES : 1) void ntt_col_db_kernel(PassArgs<TS> a) {
     using C = ColDb;
-    constexpr bool U = std::is_same<A, ArithU64>::value;
+    constexpr bool U = kIsU64<A>;
     extern __shared__ __attribute__((aligned(16))) uint64_t lds[];
     const uint32_t t = threadIdx.x, gl = t % C::NG, tau = t / C::NG, w = t >> 6, lane = t & 63;
     const uint32_t nb = a.nblocks;

@@ -354,7 +354,7 @@ struct NttPass {
         // U64 inverse block pass (MFHE_NTT_U64_INV_TWPRE, default on): the first executed stage's (w, w') pairs are loaded
         // before the entry exchange, so their latency overlaps it instead of following it (profiles/
         // r04_u64_twiddle_probe.txt: the inverse's first pass waits on these loads, the forward's passes do not)
-        constexpr bool kTwPre = INV && !COLS && std::is_same<A, ArithU64>::value && MFHE_NTT_U64_INV_TWPRE;
+        constexpr bool kTwPre = INV && !COLS && kIsU64<A> && MFHE_NTT_U64_INV_TWPRE;
         Tw wpre[kTwPre ? R / 2 : 1];
         if constexpr (kTwPre) {
             constexpr int r = NR - 1, wl = Gm::WL(r), bit = wl;   // bb = 0
@@ -378,11 +378,17 @@ struct NttPass {
                 const uint64_t twb =
                     twoff + (1ull << s) + (L.hi << (LOG_G - 1 - bit)) + (tau_hi << (LOG_R - 1 - bb));
                 if constexpr (!INV) {
+                    // first executed stage of the round: the lazy U60 policy reduces its u inputs there (a pass's
+                    // first round needs it only when the input is a raw intermediate)
+                    constexpr int fb = (LOG_R - 1 < hb - wl) ? LOG_R - 1 : hb - wl;
+                    constexpr bool first = bb == fb && (r > 0 || IN_RAW);
+                    static_assert(!kLazyU60<A> || LOG_R <= 4, "U60 bound: at most 4 stages between reductions");
 #pragma unroll
                     for (int k = 0; k < R; ++k) {
                         if (k & half) continue;
                         const Tw w = a.tw.get(twb + (uint64_t)(k >> (bb + 1)));
-                        ar.ct(x[k], x[k + half], w);
+                        if constexpr (first) ar.ct_first(x[k], x[k + half], w);
+                        else ar.ct(x[k], x[k + half], w);
                     }
                 } else {
                     // executed-stage index inside this pass (inverse rounds run r = NR-1 .. 0; only the first
@@ -480,7 +486,7 @@ struct NttPass {
                     const uint32_t g = Gm::g_of(r_store, tau_, k);
                     T y = x[k];
                     if constexpr (TWIST && INV) y = ar.mulmod(y, a.twist.get(twoff + jidx(L, g)));
-                    const uint64_t o = OUT_RAW ? A::to_raw(ar.reduce(y)) : ar.canon(y);
+                    const uint64_t o = OUT_RAW ? ar.raw_out(y) : ar.canon(y);
                     __builtin_amdgcn_raw_buffer_store_b64(__builtin_bit_cast(__attribute__((ext_vector_type(2))) unsigned, o),
                                                           rs, (int)(jidx(L, g) * 8u), 0, kCpolSt);
                 }
@@ -493,7 +499,7 @@ struct NttPass {
 #ifdef MFHE_EXP_SKIP
                     if (OUT_RAW && k >= 12) continue;   // traffic experiment only (wrong results)
 #endif
-                    L.base[jidx(L, g)] = OUT_RAW ? A::to_raw(ar.reduce(y)) : ar.canon(y);
+                    L.base[jidx(L, g)] = OUT_RAW ? ar.raw_out(y) : ar.canon(y);
                 }
             }
         }
@@ -553,7 +559,7 @@ constexpr int min_waves_per_simd(int nt) {
 #endif
 template <class A, bool COLS>
 constexpr int pass_min_waves(int nt) {
-    return (MFHE_NTT_U64_BLOCK_W4 && std::is_same<A, ArithU64>::value && !COLS && nt <= 256) ? 4 : min_waves_per_simd(nt);
+    return (MFHE_NTT_U64_BLOCK_W4 && kIsU64<A> && !COLS && nt <= 256) ? 4 : min_waves_per_simd(nt);
 }
 
 template <class A, class TS, int LOG_G, int LOG_R, int NG, bool COLS, bool INV, bool IN_RAW, bool OUT_RAW,

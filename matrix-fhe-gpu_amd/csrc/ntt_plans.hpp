@@ -102,7 +102,7 @@ static int launch_pass(const NttJob<TS>& j, int s0, hipStream_t st) {
     a.nblocks = (uint32_t)nb;
     const bool need_lds = (Gm::NR > 1) || BREV;
     const size_t lds = need_lds ? (size_t)NG * Gm::GS * sizeof(uint64_t) : 0;
-    const bool pf = j.prefetch == 1 || (MFHE_NTT_U64_BLOCK_PF && std::is_same<A, ArithU64>::value && !COLS);
+    const bool pf = j.prefetch == 1 || (MFHE_NTT_U64_BLOCK_PF && kIsU64<A> && !COLS);
     auto kern = pf ? ntt_pass_kernel<A, TS, LOG_G, LOG_R, NG, COLS, INV, IN_RAW, OUT_RAW, TWIST, BREV, UNI, true, PACK>
                    : ntt_pass_kernel<A, TS, LOG_G, LOG_R, NG, COLS, INV, IN_RAW, OUT_RAW, TWIST, BREV, UNI, false, PACK>;
     // persistent grid: resident workgroups only (occupancy query cached per instantiation), a multiple of 8
@@ -138,7 +138,7 @@ static bool col_db_usable() {
 }
 // U64 runs the single-buffer column pass (3 workgroups per CU; ntt_coldb.hpp SB), FP64 the double buffer
 template <class A>
-constexpr bool col_db_single() { return std::is_same<A, ArithU64>::value && MFHE_NTT_U64_COLDB_SB; }
+constexpr bool col_db_single() { return kIsU64<A> && MFHE_NTT_U64_COLDB_SB; }
 
 // column pass with the next tile's DMA in flight (ntt_coldb.hpp), MFHE_OPT_NTT_PREFETCH = 2: the forward's first
 // pass, or (INV) the inverse's last pass
@@ -146,7 +146,7 @@ template <class A, class TS, bool INV>
 static int launch_col_db(const NttJob<TS>& j, hipStream_t st) {
     using C = ColDb;
     constexpr bool SB = col_db_single<A>();
-    constexpr size_t lds = SB ? C::LDS_BYTES_SB_U64 : std::is_same<A, ArithU64>::value ? C::LDS_BYTES_U64 : C::LDS_BYTES;
+    constexpr size_t lds = SB ? C::LDS_BYTES_SB_U64 : kIsU64<A> ? C::LDS_BYTES_U64 : C::LDS_BYTES;
     const uint64_t npl = j.batch * (uint64_t)j.nl;
     const uint64_t nb = npl << (j.logN - C::LOG_G - C::LOG_NG);   // NG-column tiles: 2^(logN - 8) / NG per polynomial
     if (nb == 0) return MFHE_OK;
@@ -250,8 +250,18 @@ static int run_single(const NttJob<TS>& j, hipStream_t st) {
 // The batch is processed in chunks of about chunk_bytes so the raw intermediate written by pass A
 // is still resident in the Infinity Cache (256 MiB) when pass B reads and overwrites it: HBM then
 // sees ~one read and one write per element instead of two of each.
-template <class A, class TS, int LOG_GA, int NGA, int LOG_GB, int NGB, bool INV>
+// register bits per round of the U64 block passes (the FP64 ones keep 4): 16 values per thread at 4
+#ifndef MFHE_NTT_U64_BLOCK_LOGR
+#define MFHE_NTT_U64_BLOCK_LOGR 4
+#endif
+#ifndef MFHE_NTT_U64_BLOCK_NG
+#define MFHE_NTT_U64_BLOCK_NG 0   // 0: the plan's NGB
+#endif
+
+template <class A, class TS, int LOG_GA, int NGA, int LOG_GB, int NGB_, bool INV>
 static int two_pass_chunk(const NttJob<TS>& c, int pass, hipStream_t st) {
+    constexpr int RB = kIsU64<A> ? MFHE_NTT_U64_BLOCK_LOGR : 4;
+    constexpr int NGB = (kIsU64<A> && MFHE_NTT_U64_BLOCK_NG > 0) ? MFHE_NTT_U64_BLOCK_NG : NGB_;
     // pass 0 = first pass of the direction (forward: column, inverse: block), 1 = second
     constexpr bool kPackable = std::is_same<A, ArithF64>::value && LOG_GA == 8 && NGA == 16 && LOG_GB == 8 && NGB == 16;
     if constexpr (!INV && kPackable) {
@@ -267,9 +277,9 @@ static int two_pass_chunk(const NttJob<TS>& c, int pass, hipStream_t st) {
     }
     if (!INV) {
         if (pass == 0) return launch_pass<A, TS, LOG_GA, 4, NGA, true, false, false, true, false, false, true>(c, 0, st);
-        return launch_pass<A, TS, LOG_GB, 4, NGB, false, false, true, false, false, false, true>(c, LOG_GA, st);
+        return launch_pass<A, TS, LOG_GB, RB, NGB, false, false, true, false, false, false, true>(c, LOG_GA, st);
     }
-    if (pass == 0) return launch_pass<A, TS, LOG_GB, 4, NGB, false, true, false, true, false, false, true>(c, LOG_GA, st);
+    if (pass == 0) return launch_pass<A, TS, LOG_GB, RB, NGB, false, true, false, true, false, false, true>(c, LOG_GA, st);
     return launch_pass<A, TS, LOG_GA, 4, NGA, true, true, true, false, false, false, true>(c, 0, st);
 }
 
@@ -331,9 +341,10 @@ static int launch_xl2(const NttJob<TS>& j, hipStream_t st) {
     }
     a.st = c->d_xl2;
     MFHE_HIP(hipMemsetAsync(a.st, 0, words * sizeof(uint32_t), st));
-    const size_t lds = 2 * (size_t)ColDb::BUF * sizeof(uint64_t);
+    const size_t lds = 2 * ((size_t)ColDb::BUF + 4096) * sizeof(uint64_t);   // two slots: tile + B twiddles
     const uint32_t grid = (uint32_t)(j.num_cus * MFHE_XL2_WPC);
-    hipLaunchKernelGGL((ntt16_xl2_kernel<M, LAM>), dim3(grid), dim3(256), lds, st, a);
+    constexpr int LOG_R = MFHE_XL2_LOG_R;
+    hipLaunchKernelGGL((ntt16_xl2_kernel<M, LAM, LOG_R>), dim3(grid), dim3(Xl2G<LOG_R>::NT), lds, st, a);
     MFHE_CHECK_LAUNCH("ntt16_xl2_kernel launch");
     return MFHE_OK;
 }
@@ -392,5 +403,6 @@ extern template int run_kind<ArithF64, TwSrcF, false>(const NttJob<TwSrcF>&, Kin
 extern template int run_kind<ArithF64, TwSrcF, true>(const NttJob<TwSrcF>&, Kind, hipStream_t);
 extern template int run_kind<ArithU64, TwSrcU, false>(const NttJob<TwSrcU>&, Kind, hipStream_t);
 extern template int run_kind<ArithU64, TwSrcU, true>(const NttJob<TwSrcU>&, Kind, hipStream_t);
+extern template int run_kind<ArithU60, TwSrcU, false>(const NttJob<TwSrcU>&, Kind, hipStream_t);
 
 }  // namespace mfhe

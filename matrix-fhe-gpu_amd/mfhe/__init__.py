@@ -36,6 +36,7 @@ OPT_NTT_PACK = 13
 OPT_WCRT_PIPE = 14
 OPT_NTT_PLAN_EFFECTIVE = 15   # read-only: 4 pipelined single pass (2^14 FP64), 1 single pass, 2 two passes, 5 XL2
 OPT_NTT_XL2_TIMEOUT = 16      # read-only: the plan-5 kernel's sticky timeout word (synchronous)
+OPT_NTT_U60 = 17              # U64 forward with every modulus < 2^60: 1 = lazy U60 schedule (default), 0 = Harvey
 COMM_ID_BYTES = 128
 
 #: reference parameters (include/core/config.h:7-52)

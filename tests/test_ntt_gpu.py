@@ -131,6 +131,55 @@ def test_extreme_moduli_and_values_u64(mfhe, orc):
             np.testing.assert_array_equal(mfhe.to_host_u64(d), data)
 
 
+@pytest.mark.parametrize("log_n", list(range(1, 18)))
+def test_u60_forward_matches_oracle_and_harvey(mfhe, orc, log_n):
+    """The lazy U60 forward schedule (ntt_arith.hpp ArithU60: u inputs reduced once per round, unreduced
+    intermediate, FP32-quotient canonicalisation) on the largest primes below 2^60, where its 16q < 2^64 bound is
+    tightest: random, all-(q-1), all-zero and alternating inputs, bit-exact against the oracle and against the
+    Harvey schedule (MFHE_OPT_NTT_U60 0) on every plan shape log n 1..17."""
+    import torch
+    N = 1 << log_n
+    moduli = orc.gen_primes(60, 2 * N, 3)
+    assert all(2 ** 59 < q < 2 ** 60 for q in moduli)
+    ctx = mfhe.Context(moduli, log_n)
+    assert ctx.info().arith == mfhe.ARITH_U64 and ctx.get_option(mfhe.OPT_NTT_U60) == 1
+    q = np.array(moduli, np.uint64)[None, :, None]
+    rng = np.random.default_rng(60 + log_n)
+    fills = {"rand": rand_residues(rng, 2, moduli, N),
+             "max": np.broadcast_to(q - 1, (2, 3, N)).copy().ravel(),
+             "zero": np.zeros(2 * 3 * N, np.uint64),
+             "alt": np.broadcast_to(np.where(np.arange(N)[None, None, :] % 2 == 0, q - 1, 0).astype(np.uint64),
+                                    (2, 3, N)).copy().ravel()}
+    for name, data in fills.items():
+        ref = orc.phantom_fwd(data, 3, log_n, moduli)
+        outs = []
+        for u60 in (1, 0):
+            ctx.set_option(mfhe.OPT_NTT_U60, u60)
+            d = mfhe.to_device_u64(data)
+            ctx.ntt_fwd(d)
+            torch.cuda.synchronize()
+            outs.append(mfhe.to_host_u64(d))
+            np.testing.assert_array_equal(outs[-1], ref, err_msg=f"{name} u60={u60}")
+        ctx.set_option(mfhe.OPT_NTT_U60, 1)
+        d = mfhe.to_device_u64(ref)
+        ctx.ntt_inv(d)
+        torch.cuda.synchronize()
+        np.testing.assert_array_equal(mfhe.to_host_u64(d), data, err_msg=name)
+
+
+def test_u60_option_is_effective_only_below_2_60(mfhe, orc):
+    ctx = mfhe.Context(orc.gen_primes(61, 1 << 12, 2), 10)
+    assert ctx.get_option(mfhe.OPT_NTT_U60) == 0          # a modulus >= 2^60: Harvey schedule
+    ctx.set_option(mfhe.OPT_NTT_U60, 1)
+    assert ctx.get_option(mfhe.OPT_NTT_U60) == 0
+    ctx2 = mfhe.Context(orc.gen_primes(55, 1 << 12, 2), 10)
+    assert ctx2.get_option(mfhe.OPT_NTT_U60) == 1
+    ctx2.set_option(mfhe.OPT_NTT_U60, 0)
+    assert ctx2.get_option(mfhe.OPT_NTT_U60) == 0
+    with pytest.raises(mfhe.MfheError):
+        ctx2.set_option(mfhe.OPT_NTT_U60, 2)
+
+
 def test_empty_batch_is_a_no_op(mfhe, orc):
     """batch 0 (an empty ragged tail) launches nothing and touches nothing, on every plan."""
     import torch

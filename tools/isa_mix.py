@@ -28,14 +28,32 @@ def code_objects(path: str):
             r = subprocess.run([str(LLVM / "clang-offload-bundler"), "--unbundle", "--type=o", f"--input={part}",
                                 "--targets=hipv4-amdgcn-amd-amdhsa--gfx950", f"--output={co}"], capture_output=True)
             if r.returncode == 0 and co.exists() and co.stat().st_size:
-                yield subprocess.run([str(LLVM / "llvm-objdump"), "-d", str(co)], capture_output=True,
+                dis = subprocess.run([str(LLVM / "llvm-objdump"), "-d", str(co)], capture_output=True,
                                      text=True).stdout
+                notes = subprocess.run([str(LLVM / "llvm-readelf"), "--notes", str(co)], capture_output=True,
+                                       text=True).stdout
+                yield dis, kernel_meta(notes)
+
+
+def kernel_meta(notes: str):
+    """{kernel symbol: "vgpr V agpr A sgpr S scratch B lds L"} from the code object's metadata note"""
+    out = {}
+    for blk in re.split(r"\n\s+- \.", notes):
+        m = re.search(r"\.symbol:\s+(\S+)\.kd", blk)
+        if not m:
+            continue
+        f = {k: re.search(rf"\.{k}:\s+(\d+)", blk) for k in
+             ("vgpr_count", "agpr_count", "sgpr_count", "private_segment_fixed_size", "group_segment_fixed_size")}
+        v = {k: (x.group(1) if x else "?") for k, x in f.items()}
+        out[m.group(1)] = (f"vgpr {v['vgpr_count']} agpr {v['agpr_count']} sgpr {v['sgpr_count']} "
+                           f"scratch {v['private_segment_fixed_size']} lds {v['group_segment_fixed_size']}")
+    return out
 
 
 def main():
     path, pat = sys.argv[1], sys.argv[2]
     top = int(sys.argv[3]) if len(sys.argv) > 3 else 40
-    for dis in code_objects(path):
+    for dis, meta in code_objects(path):
         for m in re.finditer(r"^[0-9a-f]+ <([^>]*)>:\n(.*?)(?:\n\n|\Z)", dis, re.S | re.M):
             name = m.group(1)
             if not re.search(pat, name):
@@ -46,7 +64,7 @@ def main():
                 if ins:
                     cnt[ins.split(" ")[0]] += 1
             valu = sum(v for k, v in cnt.items() if k.startswith("v_"))
-            print(f"== {name[:150]}\n   total {sum(cnt.values())}  VALU {valu}")
+            print(f"== {name[:150]}\n   {meta.get(name, 'no metadata')}\n   total {sum(cnt.values())}  VALU {valu}")
             for k, v in sorted(cnt.items(), key=lambda kv: (not kv[0].startswith("v_"), -kv[1]))[:top]:
                 print(f"   {v:6d} {k}")
 

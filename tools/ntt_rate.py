@@ -1,6 +1,7 @@
 #!/usr/bin/env python3
 """One NTT timing line (HIP events, forward and inverse, in-place on one resident batch) for A/B runs across
-library builds (tools/lib_ab.py sets MFHE_LIB).  usage: tools/ntt_rate.py log_n L batch bits [arith] [reps]"""
+library builds (tools/lib_ab.py sets MFHE_LIB).  usage: tools/ntt_rate.py log_n L batch bits [arith] [reps] [u60]
+(u60: MFHE_OPT_NTT_U60 for the forward, default the context's)"""
 import json
 import os
 import sys
@@ -16,17 +17,21 @@ from bench import gen_moduli  # noqa: E402
 log_n, L, batch, bits = (int(x) for x in sys.argv[1:5])
 arith = int(sys.argv[5]) if len(sys.argv) > 5 else 0
 reps = int(sys.argv[6]) if len(sys.argv) > 6 else 20
+u60 = int(sys.argv[7]) if len(sys.argv) > 7 else -1
 N = 1 << log_n
 moduli = gen_moduli(bits, 1 << (log_n + 2), L)
 ctx = mfhe.Context(moduli, log_n, mfhe.CONV_PHANTOM)
 if arith:
     ctx.set_arith(arith)
+if u60 >= 0:
+    ctx.set_option(mfhe.OPT_NTT_U60, u60)
 d = torch.empty(batch * L * N, dtype=torch.int64, device="cuda")
 qt = torch.tensor(moduli, dtype=torch.int64, device="cuda").repeat_interleave(N).repeat(batch)
 d.random_(0, 2 ** 62).remainder_(qt)
 ref = d.clone()
 out = {"lib": os.path.basename(os.environ.get("MFHE_LIB", "libmfhe.so")), "log_n": log_n, "L": L, "batch": batch,
-       "bits": bits, "arith": "u64" if ctx.info().arith == mfhe.ARITH_U64 else "f64"}
+       "bits": bits, "arith": "u64" if ctx.info().arith == mfhe.ARITH_U64 else "f64",
+       "u60": ctx.get_option(mfhe.OPT_NTT_U60)}
 for kind, fn in (("fwd", ctx.ntt_fwd), ("inv", ctx.ntt_inv)):
     for _ in range(3):
         fn(d, batch=batch)
