@@ -609,6 +609,10 @@ extern "C" int mfhe_ctx_destroy(mfhe_ctx* c) {
     if (c->ws) (void)hipFree(c->ws);
     if (c->d_xl2) (void)hipFree(c->d_xl2);
     if (c->gemm_ws) (void)hipFree(c->gemm_ws);
+    if (c->gemm_ws2) (void)hipFree(c->gemm_ws2);
+    if (c->he_side) (void)hipStreamDestroy(c->he_side);
+    if (c->he_fork) (void)hipEventDestroy(c->he_fork);
+    if (c->he_join) (void)hipEventDestroy(c->he_join);
     if (c->wd_ws) (void)hipFree(c->wd_ws);
     for (void* p : c->allocs) (void)hipFree(p);
     delete c;
@@ -695,6 +699,14 @@ extern "C" int mfhe_ctx_set_option(mfhe_ctx* c, int opt, int64_t v) {
             if (v < 0 || v > 2) return set_error(MFHE_EINVAL, "trace split must be 0, 1 or 2");
             c->trace_split = (int)v;
             return MFHE_OK;
+        case MFHE_OPT_ENC_A_DIRECT:
+            if (v < 0 || v > 1) return set_error(MFHE_EINVAL, "enc a direct must be 0 or 1");
+            c->enc_a_direct = (int)v;
+            return MFHE_OK;
+        case MFHE_OPT_HE_STREAMS:
+            if (v < 0 || v > 1) return set_error(MFHE_EINVAL, "he streams must be 0 or 1");
+            c->he_streams = (int)v;
+            return MFHE_OK;
         case MFHE_OPT_NTT_U60:
             if (v < 0 || v > 1) return set_error(MFHE_EINVAL, "ntt u60 must be 0 or 1");
             c->ntt_u60 = (int)v;
@@ -751,6 +763,8 @@ extern "C" int mfhe_ctx_get_option(const mfhe_ctx* c, int opt, int64_t* v) {
         case MFHE_OPT_TRACE_SPLIT: *v = c->trace_split; return MFHE_OK;
         case MFHE_OPT_CRT_WORDS: *v = c->W; return MFHE_OK;
         case MFHE_OPT_NTT_U60: *v = c->ntt_u60 && c->u60_ok; return MFHE_OK;
+        case MFHE_OPT_HE_STREAMS: *v = c->he_streams; return MFHE_OK;
+        case MFHE_OPT_ENC_A_DIRECT: *v = c->enc_a_direct; return MFHE_OK;
         default: return set_error(MFHE_EINVAL, "unknown option");
     }
 }

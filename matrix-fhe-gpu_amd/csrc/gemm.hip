@@ -1130,7 +1130,10 @@ __device__ __forceinline__ void mfma_epilogue(const ModGemmArgs& a, const v16i (
                 const double y = 2 * u + 1 < NZ ? __fma_rn(65536.0, z[2 * u + 1], z[2 * u]) : z[2 * u];
                 v += u == 0 ? y : ar.mulmod(y, c32[u - 1]);
             }
-            Cl[(uint64_t)row * a.scM + (uint64_t)(colf >> a.log_n) * a.scY + (colf & ((1u << a.log_n) - 1))] = ar.canon(v);
+            const uint64_t o = (uint64_t)row * a.scM + (uint64_t)(colf >> a.log_n) * a.scY + (colf & ((1u << a.log_n) - 1));
+            const uint64_t cv = ar.canon(v);
+            Cl[o] = cv;
+            if (a.C2) a.C2[(uint64_t)l * a.cL + o] = cv;
         }
         return;
     }

@@ -20,6 +20,8 @@ struct ModGemmArgs {
     const uint64_t* A;     // [L][M][K] row-major, limb stride aL
     const uint64_t* B;     // limb l at B + l*bL
     uint64_t* C;           // limb l at C + l*cL
+    uint64_t* C2 = nullptr;   // factored forward only: a second copy of C, same layout (he.hip: the encrypt's shared a
+                              // written into both ciphertexts by the GEMM instead of by the ring kernel)
     uint64_t aL, bL, cL;
     uint64_t sbK, sbY, scM, scY;
     int M, K, log_n;

@@ -198,10 +198,12 @@ struct RingArgs {
 // ct_k.b = m_k - t + e, ct_k.a = a, written matrix-major; a, e poly-major.  One thread: 4 coefficients
 // of matrix row R = (w L + l) n + y.
 template <int LOGN>
+// a_mm: a is already in both ciphertexts (the W-CRT GEMM wrote it there, matrix-major): read it from aev + i0 and
+// write only the b halves -- 6 of the 8 row streams
 __global__ __launch_bounds__(256) void enc_ring_kernel(RingArgs ra, const uint64_t* __restrict__ aev,
                                                        const uint64_t* __restrict__ e, const uint64_t* __restrict__ m_re,
                                                        const uint64_t* __restrict__ m_im, uint64_t* __restrict__ ct_re,
-                                                       uint64_t* __restrict__ ct_im) {
+                                                       uint64_t* __restrict__ ct_im, int a_mm) {
     constexpr int N = 1 << LOGN, T = N / 4;
     const uint64_t g = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x;
     const int j = (int)(g % T);
@@ -215,7 +217,7 @@ __global__ __launch_bounds__(256) void enc_ring_kernel(RingArgs ra, const uint64
     const LimbConst lc = ra.lf[l];
     const ArithF64 ar(lc);
     uint64_t av[4], sk[4];
-    ld_row<LDS>(aev + p0, j, av);
+    ld_row<LDS>(aev + (a_mm ? i0 : p0), j, av);
     ld4(ra.sk + ((uint64_t)w * ra.L + l) * N + 4 * j, sk);
     // the combine's operands are loaded before the ring product (clamped rows for dead lanes), so their latency
     // overlaps the butterflies instead of following them
@@ -246,12 +248,12 @@ __global__ __launch_bounds__(256) void enc_ring_kernel(RingArgs ra, const uint64
 #pragma unroll
     for (int s = 0; s < 4; ++s) b[s] = bval(mv[s], s);
     st_row<LDS>(ct_re + i0, j, b);
-    st_row<LDS>(ct_re + total + i0, j, av);
+    if (!a_mm) st_row<LDS>(ct_re + total + i0, j, av);
     if (m_im) {
 #pragma unroll
         for (int s = 0; s < 4; ++s) b[s] = bval(mi[s], s);
         st_row<LDS>(ct_im + i0, j, b);
-        st_row<LDS>(ct_im + total + i0, j, av);
+        if (!a_mm) st_row<LDS>(ct_im + total + i0, j, av);
     }
 }
 
@@ -488,22 +490,25 @@ struct Bump {
 enum class WOut { Poly, Matrix, Vector };
 #define RC(x) do { int _r = (x); if (_r) return _r; } while (0)
 
-// i8 MFMA operands for A = V or V^-1 (gemm.hip); leaves a on the VALU kernel when unavailable
-static int use_mfma(mfhe_ctx* c, ModGemmArgs& a, const uint64_t* A, int L) {
+// i8 MFMA operands for A = V or V^-1 (gemm.hip); leaves a on the VALU kernel when unavailable.  slot 1: the side
+// stream's digit planes (HeFork)
+static int use_mfma(mfhe_ctx* c, ModGemmArgs& a, const uint64_t* A, int L, int slot = 0) {
     if (!c->wcrt_mfma || !c->wD || (A != c->d_wV && A != c->d_wVinv)) return MFHE_OK;
     const size_t need = mod_gemm_mfma_ws(a.P, L, c->wD);
-    if (c->gemm_ws_bytes < need) {
-        if (c->gemm_ws) MFHE_HIP(hipFree(c->gemm_ws));
-        c->gemm_ws = nullptr;
-        c->gemm_ws_bytes = 0;
-        MFHE_HIP(hipMalloc(&c->gemm_ws, need));
-        c->gemm_ws_bytes = need;
+    void*& ws = slot ? c->gemm_ws2 : c->gemm_ws;
+    size_t& wsb = slot ? c->gemm_ws2_bytes : c->gemm_ws_bytes;
+    if (wsb < need) {
+        if (ws) MFHE_HIP(hipFree(ws));
+        ws = nullptr;
+        wsb = 0;
+        MFHE_HIP(hipMalloc(&ws, need));
+        wsb = need;
     }
     a.Adig = A == c->d_wV ? c->d_wVdig : c->d_wVidig;
     a.adL = a.aL ? (uint64_t)c->wD * 512 * 512 : 0;
     a.D = c->wD;
     a.rtab = c->d_wrtab;
-    a.Bdig = (int8_t*)c->gemm_ws;
+    a.Bdig = (int8_t*)ws;
     // a.aL == 0: one A shared by every limb (vector transforms) -> every limb uses the full digit count
     a.limbD = (a.aL && (int)c->wDl.size() == L) ? c->wDl.data() : nullptr;
     a.epi = c->d_wepi;
@@ -533,7 +538,7 @@ static bool quant_fused_ok(const mfhe_ctx* c) {
 }
 static int wcrt_gemm(mfhe_ctx* c, const uint64_t* A, const uint64_t* B, bool b_poly, uint64_t* C, WOut out,
                      bool vector, hipStream_t s, int qsrc = 0, const double* qf = nullptr, uint64_t qf_step = 1,
-                     const RingArgs* dec = nullptr) {
+                     const RingArgs* dec = nullptr, int slot = 0, uint64_t* C2 = nullptr) {
     const Geo2 g = geo(c);
     ModGemmArgs a;
     a.A = A;
@@ -544,6 +549,7 @@ static int wcrt_gemm(mfhe_ctx* c, const uint64_t* A, const uint64_t* B, bool b_p
     a.r64 = c->d_r64;
     a.B = B;
     a.C = C;
+    a.C2 = C2;
     a.log_n = g.logn;
     if (vector) {
         a.P = (uint32_t)g.n;
@@ -556,7 +562,8 @@ static int wcrt_gemm(mfhe_ctx* c, const uint64_t* A, const uint64_t* B, bool b_p
         if (out == WOut::Poly) { a.cL = g.n; a.scM = g.n * g.L * g.n; a.scY = (uint64_t)g.L * g.n; }
         else { a.cL = g.n2; a.scM = (uint64_t)g.L * g.n2; a.scY = g.n; }
     }
-    RC(use_mfma(c, a, A, g.L));
+    RC(use_mfma(c, a, A, g.L, slot));
+    if (C2 && !a.fold) return set_error(MFHE_EINVAL, "W-CRT: a second output needs the factored forward");
     if (dec) {
         // B is the ciphertext: the factored inverse's digitize decrypts it row by row (gemm.hip
         // mfma_digitize_ifold_dec_kernel); only where dec_fused_ok(c)
@@ -654,6 +661,40 @@ static int layout(const mfhe_ctx* c, const uint64_t* in, uint64_t* out, bool to_
 }
 
 
+// Two independent chains of one call (encode's re / im W-CRT, encrypt's a / e W-CRT, decode's re / im W-INTT +
+// compose): the second runs on the context's side stream, forked from and joined back into the caller's stream by
+// events, so the digitize (memory / FP64-VALU bound) of one overlaps the i8-MFMA GEMM of the other and each GEMM's
+// tail.  The side chain's GEMM uses its own digit planes (wcrt_gemm slot 1).  MFHE_OPT_HE_STREAMS 0: x = s.
+struct HeFork {
+    hipStream_t s = nullptr, x = nullptr;
+    mfhe_ctx* c = nullptr;
+    bool on = false;
+    int begin(mfhe_ctx* c_, hipStream_t s_) {
+        c = c_;
+        s = x = s_;
+        if (!c->he_streams) return MFHE_OK;
+        if (!c->he_side) {
+            MFHE_HIP(hipStreamCreateWithFlags(&c->he_side, hipStreamNonBlocking));
+            MFHE_HIP(hipEventCreateWithFlags(&c->he_fork, hipEventDisableTiming));
+            MFHE_HIP(hipEventCreateWithFlags(&c->he_join, hipEventDisableTiming));
+        }
+        MFHE_HIP(hipEventRecord(c->he_fork, s));
+        MFHE_HIP(hipStreamWaitEvent(c->he_side, c->he_fork, 0));
+        x = c->he_side;
+        on = true;
+        return MFHE_OK;
+    }
+    // every later use of the side chain's results (and of its workspace) is ordered after this on s
+    int join() {
+        if (!on) return MFHE_OK;
+        on = false;
+        MFHE_HIP(hipEventRecord(c->he_join, x));
+        MFHE_HIP(hipStreamWaitEvent(s, c->he_join, 0));
+        return MFHE_OK;
+    }
+    ~HeFork() { (void)join(); }   // an early error return still joins the side stream into s
+};
+
 static int encode_impl(mfhe_ctx* c, const double* msg, uint64_t* out_re, uint64_t* out_im, hipStream_t s) {
     RC(need_wcrt(c));
     if (!msg || !out_re || !out_im) return set_error(MFHE_EINVAL, "mfhe_encode: null pointer");
@@ -671,9 +712,12 @@ static int encode_impl(mfhe_ctx* c, const double* msg, uint64_t* out_re, uint64_
     // 3) quantize + RNS split, 4) W-CRT -> matrix-major eval (re, then im); fused into the W-CRT's digitize
     // kernel when the factored forward runs (the residues never reach HBM)
     if (quant_fused_ok(c)) {
+        HeFork f;
+        RC(f.begin(c, s));
         RC(wcrt_gemm(c, c->d_wV, (const uint64_t*)tmp, false, out_re, WOut::Matrix, false, s, 1, (const double*)tmp, 2));
-        RC(wcrt_gemm(c, c->d_wV, (const uint64_t*)tmp, false, out_im, WOut::Matrix, false, s, 1, (const double*)tmp + 1, 2));
-        return MFHE_OK;
+        RC(wcrt_gemm(c, c->d_wV, (const uint64_t*)tmp, false, out_im, WOut::Matrix, false, f.x, 1, (const double*)tmp + 1,
+                     2, nullptr, f.on ? 1 : 0));
+        return f.join();
     }
     RC(mfhe_rns_decompose(c, (const double*)tmp, 2, 512, g.n2, cre, (mfhe_stream_t)s));
     RC(wcrt_gemm(c, c->d_wV, cre, false, out_re, WOut::Matrix, false, s));
@@ -697,11 +741,16 @@ static int decode_impl(mfhe_ctx* c, const uint64_t* ev_re, const uint64_t* ev_im
     uint64_t* coeff = pb->get<uint64_t>(g.words);
     double2* ccx = pb->get<double2>(g.cnt);
     double2* ecx = pb->get<double2>(g.cnt);
-    // W-INTT (poly-major in -> matrix-major coeff), CRT compose + centre + /delta fused, into re / im
+    // W-INTT (poly-major in -> matrix-major coeff), CRT compose + centre + /delta fused, into re / im (im on the side
+    // stream with its own coefficient buffer; the two composes write alternate doubles of ccx)
+    HeFork f;
+    RC(f.begin(c, s));
+    uint64_t* coeff_im = f.on ? pb->get<uint64_t>(g.words) : coeff;
     RC(wcrt_gemm(c, c->d_wVinv, ev_re, true, coeff, WOut::Matrix, false, s, 0, nullptr, 1, dec));
     RC(mfhe_crt_compose_f64(c, coeff, 512, g.n2, (double*)ccx, 2, (mfhe_stream_t)s));
-    RC(wcrt_gemm(c, c->d_wVinv, ev_im, true, coeff, WOut::Matrix, false, s, 0, nullptr, 1, dec));
-    RC(mfhe_crt_compose_f64(c, coeff, 512, g.n2, (double*)ccx + 1, 2, (mfhe_stream_t)s));
+    RC(wcrt_gemm(c, c->d_wVinv, ev_im, true, coeff_im, WOut::Matrix, false, f.x, 0, nullptr, 1, dec, f.on ? 1 : 0));
+    RC(mfhe_crt_compose_f64(c, coeff_im, 512, g.n2, (double*)ccx + 1, 2, (mfhe_stream_t)f.x));
+    RC(f.join());
     // W-DFT, then XY-DFT per lane: M = V E V^T
     RC(wdft(c, c->d_wdV, ccx, ecx, s));
     RC(xy3(c, c->d_encV, ecx, c->d_encVT, ccx, (double2*)msg, 512, s));
@@ -738,11 +787,16 @@ static int encrypt_impl(mfhe_ctx* c, const uint64_t* m_re, const uint64_t* m_im,
     uint64_t* ep = b.get<uint64_t>(g.words);
     uint64_t* eev = b.get<uint64_t>(g.words);
     const uint64_t W = g.words;
+    const bool a_mm = quant_fused_ok(c) && ring_fused_ok(c, g.logn) && c->enc_a_direct;
     // shared a: W coeff -> W-CRT eval (poly-major) -> X-NTT
     // e: identical for re and im (seed depends only on the coefficient, HE.cu:605-608)
     if (quant_fused_ok(c)) {
         // the samplers evaluated inside the factored W-CRT's digitize: a in place, e from one draw per coefficient
-        RC(wcrt_gemm(c, c->d_wV, ap, false, aev, WOut::Poly, false, s, 2));
+        // (e's chain on the side stream)
+        // with the fused ring: a straight into both ciphertexts' a halves (matrix-major), where enc_ring reads it
+        if (a_mm) RC(wcrt_gemm(c, c->d_wV, ap, false, ct_re + W, WOut::Matrix, false, s, 2, nullptr, 1, nullptr, 0,
+                               m_im ? ct_im + W : nullptr));
+        else RC(wcrt_gemm(c, c->d_wV, ap, false, aev, WOut::Poly, false, s, 2));
         hipLaunchKernelGGL(gaussian_compact_kernel, g1(W / g.L), dim3(256), 0, s, (double*)ep, g.logn, W / g.L);
         MFHE_CHECK_LAUNCH("gaussian_compact_kernel");
         RC(wcrt_gemm(c, c->d_wV, ep, false, eev, WOut::Poly, false, s, 3, (const double*)ep, 1));
@@ -758,7 +812,8 @@ static int encrypt_impl(mfhe_ctx* c, const uint64_t* m_re, const uint64_t* m_im,
     if (ring_fused_ok(c, g.logn)) {
         const uint64_t rows = W / g.n;
         const RingArgs ra = ring_args(c, sk, g.L, rows);
-        MFHE_RING_DISPATCH(enc_ring_kernel, g.logn, g1(rows * (g.n / 4)), s, ra, aev, eev, m_re, m_im, ct_re, ct_im);
+        MFHE_RING_DISPATCH(enc_ring_kernel, g.logn, g1(rows * (g.n / 4)), s, ra, a_mm ? ct_re + W : aev, eev, m_re, m_im,
+                           ct_re, ct_im, (int)a_mm);
         MFHE_CHECK_LAUNCH("enc_ring_kernel");
         return MFHE_OK;
     }

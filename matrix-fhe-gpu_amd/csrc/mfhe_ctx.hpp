@@ -123,6 +123,14 @@ struct mfhe_ctx {
     int limbs_total = 0;         // residue shard: L of the whole parameter set (0 = this context's L)
     void* gemm_ws = nullptr;     // B digit planes for the MFMA GEMM, grown on demand
     size_t gemm_ws_bytes = 0;
+    // MFHE_OPT_HE_STREAMS: encode / encrypt / decode run their two independent W-CRT chains (re / im, a / e) on the
+    // caller's stream and a side stream (fork / join by events); the side chain's GEMM has its own digit planes
+    int he_streams = 1;
+    int enc_a_direct = 1;         // MFHE_OPT_ENC_A_DIRECT
+    hipStream_t he_side = nullptr;
+    hipEvent_t he_fork = nullptr, he_join = nullptr;
+    void* gemm_ws2 = nullptr;
+    size_t gemm_ws2_bytes = 0;
 
     mfhe::LimbConst* d_limbs = nullptr;  // [L]
     uint64_t* d_dmod = nullptr;          // [L][3] phantom DModulus {value, const_ratio[2]}

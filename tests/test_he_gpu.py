@@ -341,18 +341,24 @@ def test_fused_ring_matches_unfused(mfhe, n, L):
     """encrypt_pair / decrypt_to_eval with the fused X-NTT * s * X-INTT row kernels (he.hip enc_ring_kernel,
     dec_ring_kernel; MFHE_OPT_HE_FUSED = 1, default) == the separate NTT / pointwise / combine kernels, bit-exact.
     decrypt_and_decode too: at n = 64 the fused path decrypts inside the inverse W-CRT's digitize (gemm.hip
-    mfma_digitize_ifold_dec_kernel), the unfused one through decrypt_to_eval and the plain digitize."""
+    mfma_digitize_ifold_dec_kernel), the unfused one through decrypt_to_eval and the plain digitize.  r05: the fused
+    encrypt with the shared a written into both ciphertexts by the W-CRT GEMM (MFHE_OPT_ENC_A_DIRECT 1, default) and
+    decode's re / im chains on two streams (MFHE_OPT_HE_STREAMS 1, default) against both off."""
     import torch
     ctx = mfhe.Context(RNS[:L], n.bit_length() - 1, CONV)
     assert ctx.get_option(mfhe.OPT_HE_FUSED) == 1
+    assert ctx.get_option(mfhe.OPT_ENC_A_DIRECT) == 1 and ctx.get_option(mfhe.OPT_HE_STREAMS) == 1
     words = 512 * L * n * n
     rng = np.random.default_rng(n + L)
     m_re, m_im = _rand_mat(rng, n, L), _rand_mat(rng, n, L)
     sk = torch.empty(512 * L * n, dtype=torch.int64, device="cuda")
     ctx.keygen(sk)
     res = {}
-    for mode in (1, 0):
+    for mode, direct, streams in ((1, 1, 1), (1, 0, 0), (0, 1, 1)):
         ctx.set_option(mfhe.OPT_HE_FUSED, mode)
+        ctx.set_option(mfhe.OPT_ENC_A_DIRECT, direct)
+        ctx.set_option(mfhe.OPT_HE_STREAMS, streams)
+        mode = (mode, direct)
         cre = torch.empty(2 * words, dtype=torch.int64, device="cuda")
         cim = torch.empty_like(cre)
         ctx.encrypt_pair(_dev(mfhe, m_re), _dev(mfhe, m_im), sk, cre, cim)
@@ -362,11 +368,12 @@ def test_fused_ring_matches_unfused(mfhe, n, L):
         ctx.decrypt_and_decode(cre, cim, sk, msg)
         torch.cuda.synchronize()
         res[mode] = [mfhe.to_host_u64(t) for t in (cre, cim, ev)] + [msg.cpu().numpy()]
-    for a, b in zip(res[1], res[0]):
-        np.testing.assert_array_equal(a, b)
+    for other in ((1, 0), (0, 1)):
+        for a, b in zip(res[(1, 1)], res[other]):
+            np.testing.assert_array_equal(a, b)
     # decrypt(encrypt(m)) = m + e: small noise around the message in the coefficient domain is checked by
     # the KAT pipelines; here the eval-domain result must differ from m_re (the encryption is not trivial)
-    assert np.mean(res[1][2] != m_re) > 0.5
+    assert np.mean(res[(1, 1)][2] != m_re) > 0.5
 
 
 def test_encode_stages_and_decode_vs_oracle(mfhe, orc, small):
@@ -469,6 +476,35 @@ def _ref_geometry_msg(pattern):
         return (v - 1j * v).ravel()
     # main.cu:62-69
     return ((ell + i * 1e-5) + 1j * (ell - i * 1e-5)).ravel()
+
+
+def test_he_streams_encode_decode_identical(mfhe):
+    """MFHE_OPT_HE_STREAMS: encode's re / im W-CRT chains and decode's W-INTT + compose chains on two streams
+    (side chain with its own digit planes and coefficient buffer) give the same words / doubles as one stream, at
+    the reference geometry, called back to back (the side stream's work of one call ordered against the next)."""
+    import torch
+    ctx = mfhe.Context(RNS, 6, CONV)
+    ctx.reserve_workspace()
+    msg = _ref_geometry_msg("encode_decode")
+    mt = torch.from_numpy(msg.view(np.float64).copy()).cuda()
+    words = 512 * 11 * 4096
+    out = {}
+    for streams in (1, 0):
+        ctx.set_option(mfhe.OPT_HE_STREAMS, streams)
+        re_ = torch.empty(words, dtype=torch.int64, device="cuda")
+        im_ = torch.empty_like(re_)
+        pre, pim = torch.empty_like(re_), torch.empty_like(re_)
+        dec = torch.empty_like(mt)
+        for _ in range(3):
+            ctx.encode(mt, re_, im_)
+            ctx.matrix_to_poly(re_, pre)
+            ctx.matrix_to_poly(im_, pim)
+            ctx.decode(pre, pim, dec)
+        torch.cuda.synchronize()
+        out[streams] = (mfhe.to_host_u64(re_), mfhe.to_host_u64(im_), dec.cpu().numpy())
+    for a, b in zip(out[1], out[0]):
+        np.testing.assert_array_equal(a, b)
+    assert np.max(np.abs(out[1][2].view(np.complex128) - msg)) < 1e-3
 
 
 def test_kat6_encode_decode_reference_geometry(mfhe):
