@@ -641,7 +641,7 @@ def cpu_baseline(log_n, moduli, seconds):
             "C1_fwd_NTT_per_s": c1r, "C2_fwd_NTT_per_s": c2r}
 
 
-def u64_line(reps=10):
+def u64_line(reps=20, warm=3):
     """C3 forward NTT on the 64-bit integer path (ArithU64, Harvey/Shoup): 60-bit primes, which the FP64 path
     cannot take (q < 2^50), and the headline's 50-bit primes forced onto U64 for comparison."""
     import torch
@@ -660,7 +660,8 @@ def u64_line(reps=10):
         del qt
         out = {}
         for kind, fn in (("fwd", ctx.ntt_fwd), ("inv", ctx.ntt_inv)):
-            fn(d, batch=batch)
+            for _ in range(warm):
+                fn(d, batch=batch)
             torch.cuda.synchronize()
             e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
             e0.record()
