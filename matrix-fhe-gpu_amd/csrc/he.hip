@@ -665,6 +665,13 @@ static int layout(const mfhe_ctx* c, const uint64_t* in, uint64_t* out, bool to_
 // compose): the second runs on the context's side stream, forked from and joined back into the caller's stream by
 // events, so the digitize (memory / FP64-VALU bound) of one overlaps the i8-MFMA GEMM of the other and each GEMM's
 // tail.  The side chain's GEMM uses its own digit planes (wcrt_gemm slot 1).  MFHE_OPT_HE_STREAMS 0: x = s.
+static int he_side_stream(mfhe_ctx* c) {   // created once (mfhe_ctx_reserve_workspace, or the first forked call)
+    if (c->he_side) return MFHE_OK;
+    MFHE_HIP(hipEventCreateWithFlags(&c->he_fork, hipEventDisableTiming));
+    MFHE_HIP(hipEventCreateWithFlags(&c->he_join, hipEventDisableTiming));
+    MFHE_HIP(hipStreamCreateWithFlags(&c->he_side, hipStreamNonBlocking));
+    return MFHE_OK;
+}
 struct HeFork {
     hipStream_t s = nullptr, x = nullptr;
     mfhe_ctx* c = nullptr;
@@ -673,11 +680,7 @@ struct HeFork {
         c = c_;
         s = x = s_;
         if (!c->he_streams) return MFHE_OK;
-        if (!c->he_side) {
-            MFHE_HIP(hipStreamCreateWithFlags(&c->he_side, hipStreamNonBlocking));
-            MFHE_HIP(hipEventCreateWithFlags(&c->he_fork, hipEventDisableTiming));
-            MFHE_HIP(hipEventCreateWithFlags(&c->he_join, hipEventDisableTiming));
-        }
+        RC(he_side_stream(c));
         MFHE_HIP(hipEventRecord(c->he_fork, s));
         MFHE_HIP(hipStreamWaitEvent(c->he_side, c->he_fork, 0));
         x = c->he_side;
@@ -899,7 +902,18 @@ using namespace mfhe;
 
 extern "C" int mfhe_ctx_reserve_workspace(mfhe_ctx* c) {
     RC(need_wcrt(c));
-    return ensure_ws(c);
+    RC(ensure_ws(c));
+    // both GEMM digit-plane workspaces (the caller's stream and the side stream of MFHE_OPT_HE_STREAMS) at the
+    // matrix transforms' size, so no W-CRT call allocates afterwards
+    if (c->wcrt_mfma && c->wD) {
+        const Geo2 g = geo(c);
+        ModGemmArgs a;
+        a.P = (uint32_t)g.n2;
+        a.aL = 512ull * 512;
+        RC(use_mfma(c, a, c->d_wV, g.L, 0));
+        RC(use_mfma(c, a, c->d_wV, g.L, 1));
+    }
+    return he_side_stream(c);
 }
 
 extern "C" int mfhe_wcrt_fwd(mfhe_ctx* c, const uint64_t* in, uint64_t* out, mfhe_stream_t s) {

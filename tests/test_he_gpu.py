@@ -507,6 +507,48 @@ def test_he_streams_encode_decode_identical(mfhe):
     assert np.max(np.abs(out[1][2].view(np.complex128) - msg)) < 1e-3
 
 
+def test_pipeline_graph_capture_replays_identically(mfhe):
+    """encode -> encrypt_pair -> decrypt_and_decode captured into one HIP graph (torch.cuda.CUDAGraph) after
+    mfhe_ctx_reserve_workspace: the side stream of MFHE_OPT_HE_STREAMS joins the capture through its fork / join
+    events and nothing allocates, so the replay writes the same words and doubles as the eager calls."""
+    import torch
+    ctx = mfhe.Context(RNS, 6, CONV)
+    ctx.reserve_workspace()
+    msg = _ref_geometry_msg("encode_decode")
+    mt = torch.from_numpy(msg.view(np.float64).copy()).cuda()
+    words = 512 * 11 * 4096
+    sk = torch.empty(512 * 11 * 64, dtype=torch.int64, device="cuda")
+    ctx.keygen(sk)
+    bufs = [torch.empty(words, dtype=torch.int64, device="cuda") for _ in range(2)]
+    cts = [torch.empty(2 * words, dtype=torch.int64, device="cuda") for _ in range(2)]
+    out = torch.empty_like(mt)
+
+    def run():
+        ctx.encode(mt, bufs[0], bufs[1])
+        ctx.encrypt_pair(bufs[0], bufs[1], sk, cts[0], cts[1])
+        ctx.decrypt_and_decode(cts[0], cts[1], sk, out)
+
+    side = torch.cuda.Stream()
+    side.wait_stream(torch.cuda.current_stream())
+    with torch.cuda.stream(side):
+        run()   # warm-up on the capture stream (lazy tables, launch attributes)
+    torch.cuda.current_stream().wait_stream(side)
+    torch.cuda.synchronize()
+    eager = [mfhe.to_host_u64(t) for t in cts] + [out.cpu().numpy()]
+    for t in cts:
+        t.zero_()
+    out.zero_()
+    g = torch.cuda.CUDAGraph()
+    with torch.cuda.graph(g):
+        run()
+    g.replay()
+    torch.cuda.synchronize()
+    got = [mfhe.to_host_u64(t) for t in cts] + [out.cpu().numpy()]
+    for a, b in zip(eager, got):
+        np.testing.assert_array_equal(a, b)
+    assert np.max(np.abs(got[2].view(np.complex128) - msg)) < 1e-3
+
+
 def test_kat6_encode_decode_reference_geometry(mfhe):
     """test_encode_decode_wcrt.cu at full reference geometry (n=64, phi=512, L=11): s = 0, a = 0."""
     import torch
