@@ -64,6 +64,35 @@ def main():
         torch.cuda.synchronize()
         res[f"{name}_ms"] = e0.elapsed_time(e1) / reps
     res["encode_encrypt_decrypt_decode_ms"] = sum(res[f"{k}_ms"] for k in ("encode", "encrypt_pair", "decrypt_and_decode"))
+
+    # the three stages back to back, eager and as one captured HIP graph (same kernels, same stream)
+    def chain():
+        stages["encode"]()
+        stages["encrypt_pair"]()
+        stages["decrypt_and_decode"]()
+    for mode in ("eager", "graph"):
+        if mode == "graph":
+            side = torch.cuda.Stream()
+            side.wait_stream(torch.cuda.current_stream())
+            with torch.cuda.stream(side):
+                chain()
+            torch.cuda.current_stream().wait_stream(side)
+            torch.cuda.synchronize()
+            g = torch.cuda.CUDAGraph()
+            with torch.cuda.graph(g):
+                chain()
+            step = g.replay
+        else:
+            step = chain
+        step()
+        torch.cuda.synchronize()
+        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        e0.record()
+        for _ in range(reps):
+            step()
+        e1.record()
+        torch.cuda.synchronize()
+        res[f"chain_{mode}_ms"] = e0.elapsed_time(e1) / reps
     err = float(np.max(np.abs(out.cpu().numpy().view(np.complex128) - msg)))
     res["max_err"] = err
     res["main_cu_check_1e-4"] = err < 1e-4
