@@ -412,6 +412,24 @@ __global__ __launch_bounds__(256) void crt_compose_f64_kernel(CrtArgs a, double 
     out[i * out_stride] = big_to_f64<W>(mag, neg, delta);
 }
 
+// two composes of the same shape in one grid (he.hip decode: re into the even doubles, im into the odd ones): blocks
+// [0, nb) compose a into oa, blocks [nb, 2 nb) compose b into ob
+template <int W>
+__global__ __launch_bounds__(256) void crt_compose_f64_pair_kernel(CrtArgs a, CrtArgs b, double delta, double* oa,
+                                                                   double* ob, uint64_t out_stride, uint32_t nb) {
+    const bool hi = blockIdx.x >= nb;
+    const CrtArgs& x = hi ? b : a;
+    const uint64_t i = (blockIdx.x - (hi ? nb : 0)) * (uint64_t)blockDim.x + threadIdx.x;
+    if (i >= x.total) return;
+    uint64_t p, c;
+    split_index(i, x.ncoeff, x.lg_nc, p, c);
+    uint64_t mag[W];
+    bool neg;
+    compose_one<W>(x.in + p * (uint64_t)x.Lg * x.ncoeff + c, x.ncoeff, x.L, x.Lg, x.shard_stride, x.qmu, x.inv,
+                   x.qinv, x.M, x.Q, x.Qh, mag, neg, x.lf, x.qbig);
+    (hi ? ob : oa)[i * out_stride] = big_to_f64<W>(mag, neg, delta);
+}
+
 template <int W>
 __global__ __launch_bounds__(256) void crt_to_f64_kernel(const uint64_t* __restrict__ mag_in,
                                                          const uint8_t* __restrict__ neg_in, uint64_t total,
@@ -528,6 +546,32 @@ extern "C" int mfhe_crt_compose_f64(mfhe_ctx* c, const uint64_t* in, size_t npol
     MFHE_CHECK_LAUNCH("crt_compose_f64_kernel");
     return MFHE_OK;
 }
+
+namespace mfhe {
+// compose a -> oa and b -> ob (same npoly, ncoeff) in one launch (he.hip decode, MFHE_OPT_HE_STREAMS 2)
+int crt_compose_f64_pair(mfhe_ctx* c, const uint64_t* a, const uint64_t* b, size_t npoly, size_t ncoeff, double* oa,
+                         double* ob, size_t out_stride, hipStream_t s) {
+    if (!c) return set_error(MFHE_EINVAL, "null ctx");
+    const uint64_t total = (uint64_t)npoly * ncoeff;
+    if (total == 0) return MFHE_OK;
+    if (!a || !b || !oa || !ob || out_stride == 0) return set_error(MFHE_EINVAL, "crt_compose_f64_pair: bad pointer/stride");
+    const CrtArgs ca = crt_args(c, a, npoly, ncoeff), cb = crt_args(c, b, npoly, ncoeff);
+    const uint64_t nb = (total + 255) / 256;
+    if (2 * nb > 0x7FFFFFFFull) return set_error(MFHE_EINVAL, "crt_compose_f64_pair: too large");
+    switch (c->W) {
+#define X(w)                                                                                                       \
+    case w:                                                                                                        \
+        hipLaunchKernelGGL(crt_compose_f64_pair_kernel<w>, dim3((uint32_t)(2 * nb)), dim3(256), 0, s, ca, cb,      \
+                           c->delta, oa, ob, (uint64_t)out_stride, (uint32_t)nb);                                  \
+        break;
+        MFHE_W_CASES(X)
+#undef X
+        default: return set_error(MFHE_EUNSUPPORTED, "crt words > 32");
+    }
+    MFHE_CHECK_LAUNCH("crt_compose_f64_pair_kernel");
+    return MFHE_OK;
+}
+}  // namespace mfhe
 
 extern "C" int mfhe_crt_to_f64(mfhe_ctx* c, const uint64_t* mag, const uint8_t* neg, size_t count, double* out,
                                size_t out_stride, mfhe_stream_t s) {

@@ -704,7 +704,7 @@ extern "C" int mfhe_ctx_set_option(mfhe_ctx* c, int opt, int64_t v) {
             c->enc_a_direct = (int)v;
             return MFHE_OK;
         case MFHE_OPT_HE_STREAMS:
-            if (v < 0 || v > 1) return set_error(MFHE_EINVAL, "he streams must be 0 or 1");
+            if (v < 0 || v > 3) return set_error(MFHE_EINVAL, "he streams must be 0, 1, 2 or 3");
             c->he_streams = (int)v;
             return MFHE_OK;
         case MFHE_OPT_NTT_U60:

@@ -538,20 +538,39 @@ struct FoldSrc {
     const uint64_t* qmu = nullptr;   // SRC 2: [L][2] (q, floor(2^64 / q))
     int lbase = 0, Ltot = 0;
 };
-template <int D, int SRC = 0>
+// PAIR (fused sources only): two components in one grid, blockIdx.x in [0, 2 L); the upper half writes fp's planes
+// from fp's source (he.hip encode: re and im)
+struct FoldPair {
+    int L = 0;
+    int8_t* out2 = nullptr;
+    uint64_t* d02 = nullptr;
+    const double* qf2 = nullptr;
+};
+template <int D, int SRC = 0, bool PAIR = false>
 __global__ __launch_bounds__(256, 4) void mfma_digitize_fold_kernel(const uint64_t* __restrict__ B, uint64_t bL,
                                                                  uint64_t sbK, uint64_t sbY, int log_n, uint32_t P,
                                                                  uint32_t Ppad, const double* __restrict__ fold,
                                                                  int8_t* __restrict__ out, uint64_t* __restrict__ d0,
-                                                                 PlaneCounts pc, FoldSrc fs = FoldSrc{}) {
+                                                                 PlaneCounts pc, FoldSrc fs = FoldSrc{},
+                                                                 FoldPair fp = FoldPair{}) {
     constexpr bool QF = SRC != 0;
+    static_assert(!PAIR || QF, "pair launches: fused sources only");
     const double* __restrict__ qf = fs.qf;
     const uint64_t qf_row = fs.qf_row, qf_step = fs.qf_step;
     const double delta = fs.delta;
     const uint32_t p = (QF ? blockIdx.y : blockIdx.x) * 128 + (threadIdx.x >> 1);
     const int hf = threadIdx.x & 1;
     const int kc = QF ? blockIdx.z : blockIdx.y;   // panel: r2 = 32 kc + 16 hf + 1 .. 32 kc + 16 hf + 16
-    const int l = QF ? blockIdx.x : blockIdx.z;
+    int lx = QF ? blockIdx.x : blockIdx.z;
+    if constexpr (PAIR) {
+        if (lx >= fp.L) {
+            lx -= fp.L;
+            out = fp.out2;
+            d0 = fp.d02;
+            qf = fp.qf2;
+        }
+    }
+    const int l = lx;
     if (p >= Ppad) return;
     const double* fo = fold + (uint64_t)l * 16;
     LimbConst lc;
@@ -795,7 +814,8 @@ __device__ __forceinline__ void ifold_finish(const ModGemmArgs& a, const ArithF6
 // Reads: ct (16 B per element) + s (L2-resident); writes: the digit planes.  The B round trip of the unfused path
 // (8 B written by dec_ring_kernel + 8 B read here per element) and one launch per component are gone.
 template <int D>
-__global__ __launch_bounds__(256, MFHE_DEC_WG_CU) void mfma_digitize_ifold_dec_kernel(ModGemmArgs a, uint32_t Ppad, PlaneCounts pc) {
+__device__ __forceinline__ void ifold_dec_impl(const ModGemmArgs& a, uint32_t Ppad, const PlaneCounts& pc, const int l,
+                                               const int L) {
     constexpr int LOGN = 6, N = 64, RS = N + 2;   // row stride 528 B: the ring's 16-B row writes spread over banks
     __shared__ __attribute__((aligned(16))) double bt[64 * RS];
 #if MFHE_DEC_RING_C
@@ -803,7 +823,6 @@ __global__ __launch_bounds__(256, MFHE_DEC_WG_CU) void mfma_digitize_ifold_dec_k
 #endif
     const int t = threadIdx.x, lane = t & 63, wv = t >> 6;
     const uint32_t y = blockIdx.x;
-    const int l = blockIdx.y, L = gridDim.y;
     typedef const __attribute__((address_space(4))) double* cdp_t;
     const cdp_t fo = (cdp_t)(a.ifold + (uint64_t)l * 16);
     LimbConst lc;
@@ -955,11 +974,22 @@ __global__ __launch_bounds__(256, MFHE_DEC_WG_CU) void mfma_digitize_ifold_dec_k
     }
     ifold_finish(a, ar, fo, e1, e2, l, Ppad, p);
 }
+template <int D>
+__global__ __launch_bounds__(256, MFHE_DEC_WG_CU) void mfma_digitize_ifold_dec_kernel(ModGemmArgs a, uint32_t Ppad, PlaneCounts pc) {
+    ifold_dec_impl<D>(a, Ppad, pc, (int)blockIdx.y, (int)gridDim.y);
+}
+// two components in one grid (he.hip decrypt_and_decode: re and im): blockIdx.y in [0, 2 L), the upper half is b
+template <int D>
+__global__ __launch_bounds__(256, MFHE_DEC_WG_CU) void mfma_digitize_ifold_dec_pair_kernel(ModGemmArgs a, ModGemmArgs b,
+                                                                                         uint32_t Ppad, PlaneCounts pc) {
+    const int L = (int)gridDim.y / 2, y = (int)blockIdx.y;
+    const bool hi = y >= L;
+    ifold_dec_impl<D>(hi ? b : a, Ppad, pc, hi ? y - L : y, L);
+}
 
 // the column sums of a split decrypt-fused digitize (gridDim.z = G shares of the panels): one thread per (column, limb)
-__global__ __launch_bounds__(256) void dec_colsum_kernel(ModGemmArgs a, uint32_t Ppad, int G) {
+__device__ __forceinline__ void dec_colsum_impl(const ModGemmArgs& a, uint32_t Ppad, int G, const int l, const int L) {
     const uint32_t p = blockIdx.x * 256 + threadIdx.x;
-    const int l = blockIdx.y, L = gridDim.y;
     if (p >= Ppad) return;
     typedef const __attribute__((address_space(4))) double* cdp_t;
     const cdp_t fo = (cdp_t)(a.ifold + (uint64_t)l * 16);
@@ -980,6 +1010,14 @@ __global__ __launch_bounds__(256) void dec_colsum_kernel(ModGemmArgs a, uint32_t
         e2[tt] = ar.reduce(e[3 + tt]);
     }
     ifold_finish(a, ar, fo, e1, e2, l, Ppad, p);
+}
+__global__ __launch_bounds__(256) void dec_colsum_kernel(ModGemmArgs a, uint32_t Ppad, int G) {
+    dec_colsum_impl(a, Ppad, G, (int)blockIdx.y, (int)gridDim.y);
+}
+__global__ __launch_bounds__(256) void dec_colsum_pair_kernel(ModGemmArgs a, ModGemmArgs b, uint32_t Ppad, int G) {
+    const int L = (int)gridDim.y / 2, y = (int)blockIdx.y;
+    const bool hi = y >= L;
+    dec_colsum_impl(hi ? b : a, Ppad, G, hi ? y - L : y, L);
 }
 
 // C = sum_s acc_s * 256^s mod q for the 32 x 32 wave tile at (m0, p0) of limb l (lane = (r, h)).
@@ -1377,6 +1415,20 @@ __global__ __launch_bounds__(256, 2) void mod_gemm_mfma_ring56_kernel(ModGemmArg
     if ((d6 >> blockIdx.z) & 1) ring_tile<6, MODE, false>(a, Ppad, l, lds);
     else ring_tile<5, MODE, false>(a, Ppad, l, lds);
 }
+// two components in one grid (blockIdx.z in [0, 2 L), the upper half is b): encode's / decode's re and im, whose
+// tiles then share the GPU without a stream fork (he.hip MFHE_OPT_HE_STREAMS 2)
+template <int MODE>
+__global__ __launch_bounds__(256, 2) void mod_gemm_mfma_ring56_pair_kernel(ModGemmArgs a, ModGemmArgs b, uint32_t Ppad,
+                                                                           uint64_t d6) {
+    constexpr int B5 = ring_lds_bytes<5, MODE>(), B6 = ring_lds_bytes<6, MODE>();
+    __shared__ __attribute__((aligned(16))) int8_t lds[B5 > B6 ? B5 : B6];
+    const int L = (int)gridDim.z / 2, z = (int)blockIdx.z;
+    const bool hi = z >= L;
+    const int l = hi ? z - L : z;
+    const ModGemmArgs& x = hi ? b : a;
+    if ((d6 >> l) & 1) ring_tile<6, MODE, false>(x, Ppad, l, lds);
+    else ring_tile<5, MODE, false>(x, Ppad, l, lds);
+}
 
 // The ring kernel's waits are counted (vmcnt(D) / vmcnt(2D): the DMAs of the stages still in flight).  A build in
 // which it spills would add scratch traffic to the counted ops; checked once per instantiation from the code
@@ -1455,6 +1507,33 @@ void balanced_digits(uint64_t x, int D, int8_t* out) {
     }
 }
 
+static FoldSrc fold_src(const ModGemmArgs& a) {
+    FoldSrc fs;
+    fs.qf = a.qf;
+    fs.qf_row = a.qf_row;
+    fs.qf_step = a.qf_step;
+    fs.delta = a.delta;
+    fs.qmu = a.qmu;
+    fs.lbase = a.lbase;
+    fs.Ltot = a.Ltot;
+    return fs;
+}
+// the factored forward's digitize from a fused source (a.qsrc 1..3) into a.Bdig / d0
+static int launch_fold_src(const ModGemmArgs& a, uint64_t* d0, int L, uint32_t Ppad, const PlaneCounts& pc,
+                           hipStream_t s) {
+    const FoldSrc fs = fold_src(a);
+    const dim3 gq(L, (Ppad + 127) / 128, FK / 32);
+#define MFHE_FOLD_SRC(d, src)                                                                                    \
+    hipLaunchKernelGGL((mfma_digitize_fold_kernel<d, src>), gq, dim3(256), 0, s, a.B, a.bL, a.sbK, a.sbY, a.log_n, \
+                       a.P, Ppad, a.fold, a.Bdig, d0, pc, fs)
+    if (a.qsrc == 1) { if (a.D == 5) MFHE_FOLD_SRC(5, 1); else MFHE_FOLD_SRC(6, 1); }
+    else if (a.qsrc == 2) { if (a.D == 5) MFHE_FOLD_SRC(5, 2); else MFHE_FOLD_SRC(6, 2); }
+    else if (a.qsrc == 3) { if (a.D == 5) MFHE_FOLD_SRC(5, 3); else MFHE_FOLD_SRC(6, 3); }
+    else return set_error(MFHE_EINVAL, "mod_gemm: unknown digitize source");
+#undef MFHE_FOLD_SRC
+    return MFHE_OK;
+}
+
 static int launch_factored(const ModGemmArgs& a, int L, hipStream_t s) {
     const uint32_t Ppad = (a.P + 63) / 64 * 64;
     ModGemmArgs f = a;
@@ -1462,23 +1541,7 @@ static int launch_factored(const ModGemmArgs& a, int L, hipStream_t s) {
     const dim3 gd((Ppad + 127) / 128, FK / 32, L);
     const PlaneCounts pc = plane_counts(a, L);
     if (a.qsrc) {
-        FoldSrc fs;
-        fs.qf = a.qf;
-        fs.qf_row = a.qf_row;
-        fs.qf_step = a.qf_step;
-        fs.delta = a.delta;
-        fs.qmu = a.qmu;
-        fs.lbase = a.lbase;
-        fs.Ltot = a.Ltot;
-        const dim3 gq(L, (Ppad + 127) / 128, FK / 32);
-#define MFHE_FOLD_SRC(d, src)                                                                                    \
-    hipLaunchKernelGGL((mfma_digitize_fold_kernel<d, src>), gq, dim3(256), 0, s, a.B, a.bL, a.sbK, a.sbY, a.log_n, \
-                       a.P, Ppad, a.fold, a.Bdig, f.d0, pc, fs)
-        if (a.qsrc == 1) { if (a.D == 5) MFHE_FOLD_SRC(5, 1); else MFHE_FOLD_SRC(6, 1); }
-        else if (a.qsrc == 2) { if (a.D == 5) MFHE_FOLD_SRC(5, 2); else MFHE_FOLD_SRC(6, 2); }
-        else if (a.qsrc == 3) { if (a.D == 5) MFHE_FOLD_SRC(5, 3); else MFHE_FOLD_SRC(6, 3); }
-        else return set_error(MFHE_EINVAL, "mod_gemm: unknown digitize source");
-#undef MFHE_FOLD_SRC
+        if (int rc = launch_fold_src(a, f.d0, L, Ppad, pc, s)) return rc;
     } else if (a.D == 5) {
         hipLaunchKernelGGL(mfma_digitize_fold_kernel<5>, gd, dim3(256), 0, s, a.B, a.bL, a.sbK, a.sbY, a.log_n,
                            a.P, Ppad, a.fold, a.Bdig, f.d0, pc);
@@ -1548,6 +1611,98 @@ static int launch_factored_inv(const ModGemmArgs& a, int L, hipStream_t s) {
         MFHE_CHECK_LAUNCH("mod_gemm_mfma kernel (factored inverse)");
         l0 = l1;
     }
+    return MFHE_OK;
+}
+
+static bool ring56_all(const ModGemmArgs& f, int L, uint64_t& d6) {
+    d6 = 0;
+    if (f.pipe != 0 || L > 64) return false;
+    for (int l = 0; l < L; ++l) {
+        const int d = f.limbD ? std::max(f.limbD[l], 5) : f.D;
+        if (d != 5 && d != 6) return false;
+        if (d == 6) d6 |= 1ull << l;
+    }
+    return true;
+}
+template <int MODE>
+static bool ring56_pair_usable() {
+    static int ok = -1;
+    if (ok < 0) {
+        hipFuncAttributes fa{};
+        ok = hipFuncGetAttributes(&fa, reinterpret_cast<const void*>(mod_gemm_mfma_ring56_pair_kernel<MODE>)) ==
+                     hipSuccess &&
+             fa.localSizeBytes == 0;
+    }
+    return ok == 1;
+}
+
+// Two independent W-CRT transforms of the same shape (encode's re / im from the W-IDFT's doubles, decode's decrypt-fused
+// re / im) as one launch per step: digitize pair, (column sums pair), ring56 GEMM pair -- grids of 2 L limbs, the upper
+// half the second component.  Their workgroups share the GPU without a stream fork and its event waits (8-13 us of
+// idle per fork or join, profiles/r05_pipeline_chain_trace.txt).  Anything else runs the two sequentially.
+int launch_mod_gemm_pair(const ModGemmArgs& a, const ModGemmArgs& b, int L, hipStream_t s) {
+    const uint32_t Ppad = (a.P + 63) / 64 * 64;
+    uint64_t d6a = 0, d6b = 0;
+    const bool inv = a.Adig && a.ifold && a.dct && b.Adig && b.ifold && b.dct && ring56_pair_usable<2>();
+    const bool fwd = a.Adig && a.fold && a.qsrc && b.Adig && b.fold && b.qsrc && ring56_pair_usable<1>();
+    const bool same = a.P == b.P && a.D == b.D && a.M == 512 && a.K == MK && a.epi && b.epi && a.lds_stage &&
+                      a.D >= 5 && a.D <= 6 && 2 * L <= 128 && ring56_all(a, L, d6a) && ring56_all(b, L, d6b) &&
+                      d6a == d6b;
+    if (!(inv || fwd) || !same || (inv && (a.log_n != 6 || a.P != 64u * 64u || Ppad != a.P || !a.iz || !a.phi))) {
+        if (int rc = launch_mod_gemm(a, L, s)) return rc;
+        return launch_mod_gemm(b, L, s);
+    }
+    const PlaneCounts pc = plane_counts(a, L);
+    ModGemmArgs f[2] = {a, b};
+    const dim3 gg(2 * Ppad / 64, FK / 64, 2 * L);
+    if (inv) {
+        constexpr int G = MFHE_DEC_SPLIT;
+        for (auto& x : f) {
+            if (!x.dsk || !x.dlf || !x.dtw || !x.ditw || !x.dninv)
+                return set_error(MFHE_EINVAL, "mod_gemm: the decrypt-fused inverse W-CRT needs the ring tables");
+            x.cc = (double*)(x.Bdig + (size_t)L * x.D * Ppad * MK);
+            x.dpart = x.cc + (size_t)L * Ppad * 2;
+        }
+        const dim3 gr(64, 2 * L, G);
+        if (a.D == 5) hipLaunchKernelGGL(mfma_digitize_ifold_dec_pair_kernel<5>, gr, dim3(256), 0, s, f[0], f[1], Ppad, pc);
+        else hipLaunchKernelGGL(mfma_digitize_ifold_dec_pair_kernel<6>, gr, dim3(256), 0, s, f[0], f[1], Ppad, pc);
+        MFHE_CHECK_LAUNCH("mfma_digitize_ifold_dec_pair_kernel");
+        if (G > 1) {
+            hipLaunchKernelGGL(dec_colsum_pair_kernel, dim3((Ppad + 255) / 256, 2 * L), dim3(256), 0, s, f[0], f[1], Ppad, G);
+            MFHE_CHECK_LAUNCH("dec_colsum_pair_kernel");
+        }
+        hipLaunchKernelGGL(mod_gemm_mfma_ring56_pair_kernel<2>, gg, dim3(256), 0, s, f[0], f[1], Ppad, d6a);
+        MFHE_CHECK_LAUNCH("mod_gemm_mfma_ring56_pair_kernel (factored inverse)");
+        return MFHE_OK;
+    }
+    for (auto& x : f) x.d0 = (uint64_t*)(x.Bdig + (size_t)L * x.D * Ppad * MK);
+    // the two digitizes: one launch when both read the same doubles' rows (encode's re / im), else one each (the
+    // encrypt's uniform a and Gaussian e)
+    if (!(a.qsrc == 1 && b.qsrc == 1 && a.B == b.B && a.qf_row == b.qf_row && a.qf_step == b.qf_step &&
+          a.delta == b.delta)) {
+        for (const auto& x : f)
+            if (int rc = launch_fold_src(x, x.d0, L, Ppad, pc, s)) return rc;
+        MFHE_CHECK_LAUNCH("mfma_digitize_fold_kernel");
+        hipLaunchKernelGGL(mod_gemm_mfma_ring56_pair_kernel<1>, gg, dim3(256), 0, s, f[0], f[1], Ppad, d6a);
+        MFHE_CHECK_LAUNCH("mod_gemm_mfma_ring56_pair_kernel (factored)");
+        return MFHE_OK;
+    }
+    const FoldSrc fs = fold_src(a);
+    FoldPair fp;
+    fp.L = L;
+    fp.out2 = f[1].Bdig;
+    fp.d02 = f[1].d0;
+    fp.qf2 = b.qf;
+    const dim3 gq(2 * L, (Ppad + 127) / 128, FK / 32);
+#define MFHE_FOLD_PAIR(d, src)                                                                                     \
+    hipLaunchKernelGGL((mfma_digitize_fold_kernel<d, src, true>), gq, dim3(256), 0, s, a.B, a.bL, a.sbK, a.sbY,   \
+                       a.log_n, a.P, Ppad, a.fold, f[0].Bdig, f[0].d0, pc, fs, fp)
+    if (a.D == 5) MFHE_FOLD_PAIR(5, 1);
+    else MFHE_FOLD_PAIR(6, 1);
+#undef MFHE_FOLD_PAIR
+    MFHE_CHECK_LAUNCH("mfma_digitize_fold_kernel (pair)");
+    hipLaunchKernelGGL(mod_gemm_mfma_ring56_pair_kernel<1>, gg, dim3(256), 0, s, f[0], f[1], Ppad, d6a);
+    MFHE_CHECK_LAUNCH("mod_gemm_mfma_ring56_pair_kernel (factored)");
     return MFHE_OK;
 }
 

@@ -101,6 +101,8 @@ struct CGemmArgs {
 };
 
 int launch_mod_gemm(const ModGemmArgs& a, int L, hipStream_t s);
+// two independent W-CRT transforms of the same shape as one launch per step (gemm.hip; he.hip encode / decode)
+int launch_mod_gemm_pair(const ModGemmArgs& a, const ModGemmArgs& b, int L, hipStream_t s);
 int launch_cgemm(const CGemmArgs& a, int batch, hipStream_t s);
 // factored inverse W-DFT, first step: per column the rows r2 = 0, 255, 256 of E_a by dot products (xpow [2][256]:
 // zeta^(-255 b), zeta^(-256 b)), then f_0, f_257 into out and (c0, c1) into a.cc (gemm.hip)

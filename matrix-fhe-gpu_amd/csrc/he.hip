@@ -21,6 +21,9 @@ extern "C" int mfhe_ntt_fwd(mfhe_ctx*, uint64_t*, size_t, int, int, mfhe_stream_
 extern "C" int mfhe_ntt_inv(mfhe_ctx*, uint64_t*, size_t, int, int, mfhe_stream_t);
 extern "C" int mfhe_crt_compose(mfhe_ctx*, const uint64_t*, size_t, size_t, uint64_t*, uint8_t*, mfhe_stream_t);
 extern "C" int mfhe_crt_compose_f64(mfhe_ctx*, const uint64_t*, size_t, size_t, double*, size_t, mfhe_stream_t);
+namespace mfhe {
+int crt_compose_f64_pair(mfhe_ctx*, const uint64_t*, const uint64_t*, size_t, size_t, double*, double*, size_t, hipStream_t);
+}
 extern "C" int mfhe_rns_decompose(mfhe_ctx*, const double*, size_t, size_t, size_t, uint64_t*, mfhe_stream_t);
 
 namespace mfhe {
@@ -536,11 +539,12 @@ static int use_mfma(mfhe_ctx* c, ModGemmArgs& a, const uint64_t* A, int L, int s
 static bool quant_fused_ok(const mfhe_ctx* c) {
     return c->wcrt_mfma == 1 && c->wD && c->d_wZdig && c->d_wepi && c->d_wfold;
 }
-static int wcrt_gemm(mfhe_ctx* c, const uint64_t* A, const uint64_t* B, bool b_poly, uint64_t* C, WOut out,
-                     bool vector, hipStream_t s, int qsrc = 0, const double* qf = nullptr, uint64_t qf_step = 1,
+// the GEMM arguments of one W-CRT transform (wcrt_gemm launches them; encode / decode may launch two of them as
+// pairs, gemm.hip launch_mod_gemm_pair)
+static int wcrt_args(mfhe_ctx* c, ModGemmArgs& a, const uint64_t* A, const uint64_t* B, bool b_poly, uint64_t* C,
+                     WOut out, bool vector, int qsrc = 0, const double* qf = nullptr, uint64_t qf_step = 1,
                      const RingArgs* dec = nullptr, int slot = 0, uint64_t* C2 = nullptr) {
     const Geo2 g = geo(c);
-    ModGemmArgs a;
     a.A = A;
     a.aL = 512ull * 512;
     a.M = 512;
@@ -586,7 +590,14 @@ static int wcrt_gemm(mfhe_ctx* c, const uint64_t* A, const uint64_t* B, bool b_p
         a.lbase = c->limb_base;
         a.Ltot = c->limbs_total ? c->limbs_total : g.L;
     }
-    return launch_mod_gemm(a, g.L, s);
+    return MFHE_OK;
+}
+static int wcrt_gemm(mfhe_ctx* c, const uint64_t* A, const uint64_t* B, bool b_poly, uint64_t* C, WOut out,
+                     bool vector, hipStream_t s, int qsrc = 0, const double* qf = nullptr, uint64_t qf_step = 1,
+                     const RingArgs* dec = nullptr, int slot = 0, uint64_t* C2 = nullptr) {
+    ModGemmArgs a;
+    RC(wcrt_args(c, a, A, B, b_poly, C, out, vector, qsrc, qf, qf_step, dec, slot, C2));
+    return launch_mod_gemm(a, c->L, s);
 }
 
 // complex W-DFT / W-IDFT over [phi][n2]; MFHE_OPT_CGEMM_MFMA = 2 (default): factored through 771 = 3 x 257
@@ -676,10 +687,10 @@ struct HeFork {
     hipStream_t s = nullptr, x = nullptr;
     mfhe_ctx* c = nullptr;
     bool on = false;
-    int begin(mfhe_ctx* c_, hipStream_t s_) {
+    int begin(mfhe_ctx* c_, hipStream_t s_, bool enable) {
         c = c_;
         s = x = s_;
-        if (!c->he_streams) return MFHE_OK;
+        if (!enable) return MFHE_OK;
         RC(he_side_stream(c));
         MFHE_HIP(hipEventRecord(c->he_fork, s));
         MFHE_HIP(hipStreamWaitEvent(c->he_side, c->he_fork, 0));
@@ -715,8 +726,15 @@ static int encode_impl(mfhe_ctx* c, const double* msg, uint64_t* out_re, uint64_
     // 3) quantize + RNS split, 4) W-CRT -> matrix-major eval (re, then im); fused into the W-CRT's digitize
     // kernel when the factored forward runs (the residues never reach HBM)
     if (quant_fused_ok(c)) {
+        if (c->he_streams >= 2) {   // modes 2, 3: re and im as one launch per step (gemm.hip launch_mod_gemm_pair)
+            ModGemmArgs ar, ai;
+            RC(wcrt_args(c, ar, c->d_wV, (const uint64_t*)tmp, false, out_re, WOut::Matrix, false, 1, (const double*)tmp, 2));
+            RC(wcrt_args(c, ai, c->d_wV, (const uint64_t*)tmp, false, out_im, WOut::Matrix, false, 1, (const double*)tmp + 1,
+                         2, nullptr, 1));
+            return launch_mod_gemm_pair(ar, ai, g.L, s);
+        }
         HeFork f;
-        RC(f.begin(c, s));
+        RC(f.begin(c, s, c->he_streams == 1));
         RC(wcrt_gemm(c, c->d_wV, (const uint64_t*)tmp, false, out_re, WOut::Matrix, false, s, 1, (const double*)tmp, 2));
         RC(wcrt_gemm(c, c->d_wV, (const uint64_t*)tmp, false, out_im, WOut::Matrix, false, f.x, 1, (const double*)tmp + 1,
                      2, nullptr, f.on ? 1 : 0));
@@ -746,8 +764,19 @@ static int decode_impl(mfhe_ctx* c, const uint64_t* ev_re, const uint64_t* ev_im
     double2* ecx = pb->get<double2>(g.cnt);
     // W-INTT (poly-major in -> matrix-major coeff), CRT compose + centre + /delta fused, into re / im (im on the side
     // stream with its own coefficient buffer; the two composes write alternate doubles of ccx)
+    if (c->he_streams == 2) {
+        // re and im as one launch per step: W-INTT pair (gemm.hip launch_mod_gemm_pair), then one compose launch
+        uint64_t* coeff_im = pb->get<uint64_t>(g.words);
+        ModGemmArgs ar, ai;
+        RC(wcrt_args(c, ar, c->d_wVinv, ev_re, true, coeff, WOut::Matrix, false, 0, nullptr, 1, dec));
+        RC(wcrt_args(c, ai, c->d_wVinv, ev_im, true, coeff_im, WOut::Matrix, false, 0, nullptr, 1, dec, 1));
+        RC(launch_mod_gemm_pair(ar, ai, g.L, s));
+        RC(crt_compose_f64_pair(c, coeff, coeff_im, 512, g.n2, (double*)ccx, (double*)ccx + 1, 2, s));
+        RC(wdft(c, c->d_wdV, ccx, ecx, s));
+        return xy3(c, c->d_encV, ecx, c->d_encVT, ccx, (double2*)msg, 512, s);
+    }
     HeFork f;
-    RC(f.begin(c, s));
+    RC(f.begin(c, s, c->he_streams == 1 || c->he_streams == 3));
     uint64_t* coeff_im = f.on ? pb->get<uint64_t>(g.words) : coeff;
     RC(wcrt_gemm(c, c->d_wVinv, ev_re, true, coeff, WOut::Matrix, false, s, 0, nullptr, 1, dec));
     RC(mfhe_crt_compose_f64(c, coeff, 512, g.n2, (double*)ccx, 2, (mfhe_stream_t)s));
@@ -794,15 +823,21 @@ static int encrypt_impl(mfhe_ctx* c, const uint64_t* m_re, const uint64_t* m_im,
     // shared a: W coeff -> W-CRT eval (poly-major) -> X-NTT
     // e: identical for re and im (seed depends only on the coefficient, HE.cu:605-608)
     if (quant_fused_ok(c)) {
-        // the samplers evaluated inside the factored W-CRT's digitize: a in place, e from one draw per coefficient
-        // (e's chain on the side stream)
-        // with the fused ring: a straight into both ciphertexts' a halves (matrix-major), where enc_ring reads it
-        if (a_mm) RC(wcrt_gemm(c, c->d_wV, ap, false, ct_re + W, WOut::Matrix, false, s, 2, nullptr, 1, nullptr, 0,
+        // the samplers evaluated inside the factored W-CRT's digitize: a in place, e from one draw per coefficient;
+        // with the fused ring, a straight into both ciphertexts' a halves (matrix-major), where enc_ring reads it.
+        // MFHE_OPT_HE_STREAMS 2: the two GEMMs as one launch (gemm.hip launch_mod_gemm_pair; measured no faster than
+        // two: 301 vs 160 + 138 us, profiles/r05_he_stream_modes.txt, so mode 3 keeps two)
+        const bool pair = c->he_streams == 2;
+        ModGemmArgs aa, ae;
+        if (a_mm) RC(wcrt_args(c, aa, c->d_wV, ap, false, ct_re + W, WOut::Matrix, false, 2, nullptr, 1, nullptr, 0,
                                m_im ? ct_im + W : nullptr));
-        else RC(wcrt_gemm(c, c->d_wV, ap, false, aev, WOut::Poly, false, s, 2));
+        else RC(wcrt_args(c, aa, c->d_wV, ap, false, aev, WOut::Poly, false, 2));
+        RC(wcrt_args(c, ae, c->d_wV, ep, false, eev, WOut::Poly, false, 3, (const double*)ep, 1, nullptr, pair ? 1 : 0));
+        if (!pair) RC(launch_mod_gemm(aa, g.L, s));
         hipLaunchKernelGGL(gaussian_compact_kernel, g1(W / g.L), dim3(256), 0, s, (double*)ep, g.logn, W / g.L);
         MFHE_CHECK_LAUNCH("gaussian_compact_kernel");
-        RC(wcrt_gemm(c, c->d_wV, ep, false, eev, WOut::Poly, false, s, 3, (const double*)ep, 1));
+        if (pair) RC(launch_mod_gemm_pair(aa, ae, g.L, s));
+        else RC(launch_mod_gemm(ae, g.L, s));
     } else {
         hipLaunchKernelGGL(uniform_kernel, g1(W), dim3(256), 0, s, ap, c->d_rns_mu, g.L, g.logn, W, c->limb_base,
                            c->limbs_total ? c->limbs_total : g.L);

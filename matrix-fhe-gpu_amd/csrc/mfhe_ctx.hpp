@@ -123,9 +123,10 @@ struct mfhe_ctx {
     int limbs_total = 0;         // residue shard: L of the whole parameter set (0 = this context's L)
     void* gemm_ws = nullptr;     // B digit planes for the MFMA GEMM, grown on demand
     size_t gemm_ws_bytes = 0;
-    // MFHE_OPT_HE_STREAMS: encode / encrypt / decode run their two independent W-CRT chains (re / im, a / e) on the
-    // caller's stream and a side stream (fork / join by events); the side chain's GEMM has its own digit planes
-    int he_streams = 1;
+    // MFHE_OPT_HE_STREAMS (include/mfhe.h): how encode / decode run their two independent W-CRT chains (re / im):
+    // side stream (fork / join by events) or one grid per step over both components; the second component's GEMM
+    // has its own digit planes
+    int he_streams = 3;
     int enc_a_direct = 1;         // MFHE_OPT_ENC_A_DIRECT
     hipStream_t he_side = nullptr;
     hipEvent_t he_fork = nullptr, he_join = nullptr;

@@ -347,18 +347,18 @@ def test_fused_ring_matches_unfused(mfhe, n, L):
     import torch
     ctx = mfhe.Context(RNS[:L], n.bit_length() - 1, CONV)
     assert ctx.get_option(mfhe.OPT_HE_FUSED) == 1
-    assert ctx.get_option(mfhe.OPT_ENC_A_DIRECT) == 1 and ctx.get_option(mfhe.OPT_HE_STREAMS) == 1
+    assert ctx.get_option(mfhe.OPT_ENC_A_DIRECT) == 1 and ctx.get_option(mfhe.OPT_HE_STREAMS) == 3
     words = 512 * L * n * n
     rng = np.random.default_rng(n + L)
     m_re, m_im = _rand_mat(rng, n, L), _rand_mat(rng, n, L)
     sk = torch.empty(512 * L * n, dtype=torch.int64, device="cuda")
     ctx.keygen(sk)
     res = {}
-    for mode, direct, streams in ((1, 1, 1), (1, 0, 0), (0, 1, 1)):
+    for mode, direct, streams in ((1, 1, 1), (1, 0, 0), (0, 1, 1), (1, 1, 2)):
         ctx.set_option(mfhe.OPT_HE_FUSED, mode)
         ctx.set_option(mfhe.OPT_ENC_A_DIRECT, direct)
         ctx.set_option(mfhe.OPT_HE_STREAMS, streams)
-        mode = (mode, direct)
+        mode = (mode, direct) if streams != 2 else (mode, direct, 2)
         cre = torch.empty(2 * words, dtype=torch.int64, device="cuda")
         cim = torch.empty_like(cre)
         ctx.encrypt_pair(_dev(mfhe, m_re), _dev(mfhe, m_im), sk, cre, cim)
@@ -368,7 +368,7 @@ def test_fused_ring_matches_unfused(mfhe, n, L):
         ctx.decrypt_and_decode(cre, cim, sk, msg)
         torch.cuda.synchronize()
         res[mode] = [mfhe.to_host_u64(t) for t in (cre, cim, ev)] + [msg.cpu().numpy()]
-    for other in ((1, 0), (0, 1)):
+    for other in ((1, 0), (0, 1), (1, 1, 2)):
         for a, b in zip(res[(1, 1)], res[other]):
             np.testing.assert_array_equal(a, b)
     # decrypt(encrypt(m)) = m + e: small noise around the message in the coefficient domain is checked by
@@ -480,8 +480,9 @@ def _ref_geometry_msg(pattern):
 
 def test_he_streams_encode_decode_identical(mfhe):
     """MFHE_OPT_HE_STREAMS: encode's re / im W-CRT chains and decode's W-INTT + compose chains on two streams
-    (side chain with its own digit planes and coefficient buffer) give the same words / doubles as one stream, at
-    the reference geometry, called back to back (the side stream's work of one call ordered against the next)."""
+    (1: side chain with its own digit planes and coefficient buffer) or as one launch per step with grids over both
+    components (2: gemm.hip launch_mod_gemm_pair, the pair kernels) give the same words / doubles as one plain stream
+    (0), at the reference geometry, called back to back."""
     import torch
     ctx = mfhe.Context(RNS, 6, CONV)
     ctx.reserve_workspace()
@@ -489,7 +490,7 @@ def test_he_streams_encode_decode_identical(mfhe):
     mt = torch.from_numpy(msg.view(np.float64).copy()).cuda()
     words = 512 * 11 * 4096
     out = {}
-    for streams in (1, 0):
+    for streams in (1, 2, 3, 0):
         ctx.set_option(mfhe.OPT_HE_STREAMS, streams)
         re_ = torch.empty(words, dtype=torch.int64, device="cuda")
         im_ = torch.empty_like(re_)
@@ -502,8 +503,9 @@ def test_he_streams_encode_decode_identical(mfhe):
             ctx.decode(pre, pim, dec)
         torch.cuda.synchronize()
         out[streams] = (mfhe.to_host_u64(re_), mfhe.to_host_u64(im_), dec.cpu().numpy())
-    for a, b in zip(out[1], out[0]):
-        np.testing.assert_array_equal(a, b)
+    for other in (2, 3, 0):
+        for a, b in zip(out[1], out[other]):
+            np.testing.assert_array_equal(a, b)
     assert np.max(np.abs(out[1][2].view(np.complex128) - msg)) < 1e-3
 
 
