@@ -1038,8 +1038,11 @@ __global__ __launch_bounds__(256) void dec_colsum_pair_kernel(ModGemmArgs a, Mod
 // parts of the same 64-byte groups: their workgroups are given block ids on one XCD (the L2 that merges them).
 // F[w][digit][m], m = k - x + 63: s[63 - m] (m <= 63), -s[127 - m] (m > 63): lane (x, g) needs the 16 bytes
 // F[16 g - x + 63 ..], read as five dwords and funnel-shifted (v_alignbyte) by its offset mod 4.
+#ifndef MFHE_DMM_KW
+#define MFHE_DMM_KW 16   // w per dec_mm_digitize_kernel workgroup: 16 (a quarter) or 8 (half of one, 2 workgroups / CU)
+#endif
 #ifndef MFHE_DMM_WG_CU
-#define MFHE_DMM_WG_CU 1   // dec_mm_digitize_kernel workgroups per CU (launch bound; the LDS stage allows one)
+#define MFHE_DMM_WG_CU (MFHE_DMM_KW == 16 ? 1 : 2)   // launch bound (the LDS stage allows one at 16 w)
 #endif
 #ifndef MFHE_DMM_AHEAD
 #define MFHE_DMM_AHEAD 3   // iterations of lookahead of dec_mm_digitize_kernel's loads (1 or 3)
@@ -1048,16 +1051,19 @@ __global__ __launch_bounds__(256) void dec_colsum_pair_kernel(ModGemmArgs a, Mod
 #define MFHE_DMM_SCHED 1
 #endif
 constexpr int DMM_RS = 80;   // A tile row stride in bytes (16 B of padding: rows of one read spread over banks)
+constexpr int DMM_KW = MFHE_DMM_KW;
+static_assert(DMM_KW == 16 || DMM_KW == 8, "16 or 8 w per workgroup");
 template <int D>
 __device__ __forceinline__ void dec_mm_impl(const ModGemmArgs& a, uint32_t Ppad, const PlaneCounts& pc, const int l,
-                                            const int L, const int kc, const int ap, const int hf, const int yg) {
-    constexpr int N = 64, NS = 2 * D - 1, NZ = (NS + 1) / 2, NY = (NZ + 1) / 2;
-    __shared__ __attribute__((aligned(16))) uint32_t ftab[16][D][32];
+                                            const int L, const int kc, const int ap, const int hf, const int yg,
+                                            const int half) {
+    constexpr int N = 64, NS = 2 * D - 1, NZ = (NS + 1) / 2, NY = (NZ + 1) / 2, KW = DMM_KW;
+    __shared__ __attribute__((aligned(16))) uint32_t ftab[KW][D][32];
     __shared__ __attribute__((aligned(16))) uint32_t atab[2][D][16][DMM_RS / 4];
     // the digit bytes of this quarter: [plane][column of the workgroup][16 k], written out once at the end so each
     // 64-byte group is completed by the four quarters' workgroups at about the same time (4-byte stores spread over
     // the kernel's life left partial lines to be evicted: 3-4x slower)
-    __shared__ __attribute__((aligned(16))) uint32_t dstage[D][1024][4];
+    __shared__ __attribute__((aligned(16))) uint32_t dstage[D][1024][KW / 4];
     const int t = threadIdx.x, lane = t & 63, wv = t >> 6;
     typedef const __attribute__((address_space(4))) double* cdp_t;
     const cdp_t fo = (cdp_t)(a.ifold + (uint64_t)l * 16);
@@ -1070,37 +1076,37 @@ __device__ __forceinline__ void dec_mm_impl(const ModGemmArgs& a, uint32_t Ppad,
     const double c32[3] = {ep[2], ep[3], ep[4]};
     const cdp_t izl = (cdp_t)(a.iz + (uint64_t)l * 48);
     const double x1 = izl[0], x2 = izl[1];
-    const uint64_t w0 = (uint64_t)ap * FK + kc * 32 + hf * 16;   // w of kk = 0
+    const uint64_t w0 = (uint64_t)ap * FK + kc * 32 + hf * 16 + half * 8;   // w of kk = 0
     const uint64_t* __restrict__ cta = a.dct + a.dtotal;
-    // F tables of the 16 w: thread (kk, 8 entries)
+    // F tables of the KW w: thread (kk, EPT entries)
     {
-        const int kk = t >> 4, m0 = (t & 15) * 8;
+        constexpr int TPW = 256 / KW, EPT = 128 / TPW;
+        const int kk = t / TPW, m0 = (t % TPW) * EPT;
         const uint64_t* sc = a.dskc + ((w0 + kk) * L + l) * N;
-        uint32_t lo[D], hi[D];
+        uint32_t dw[D][EPT / 4];
 #pragma unroll
-        for (int i = 0; i < D; ++i) lo[i] = hi[i] = 0;
-        uint64_t sv[8];
+        for (int i = 0; i < D; ++i)
 #pragma unroll
-        for (int e = 0; e < 8; ++e) {   // every load unconditional (a load under a branch waits at once)
+            for (int c = 0; c < EPT / 4; ++c) dw[i][c] = 0;
+        uint64_t sv[EPT];
+#pragma unroll
+        for (int e = 0; e < EPT; ++e) {   // every load unconditional (a load under a branch waits at once)
             const int m = m0 + e;
             sv[e] = sc[m <= 63 ? 63 - m : (m <= 126 ? 127 - m : 0)];
         }
 #pragma unroll
-        for (int e = 0; e < 8; ++e) {
+        for (int e = 0; e < EPT; ++e) {
             const int m = m0 + e;
             const double c = centred_f(sv[e], q);
             const double v = m <= 63 ? c : (m <= 126 ? -c : 0.0);
             const uint64_t bb = balanced_bytes<D>(v);
 #pragma unroll
-            for (int i = 0; i < D; ++i) {
-                const uint32_t by = ((uint32_t)(bb >> (8 * i)) & 255u) << (8 * (e & 3));
-                if (e < 4) lo[i] |= by;
-                else hi[i] |= by;
-            }
+            for (int i = 0; i < D; ++i) dw[i][e >> 2] |= ((uint32_t)(bb >> (8 * i)) & 255u) << (8 * (e & 3));
         }
 #pragma unroll
         for (int i = 0; i < D; ++i)
-            *(uint2*)&ftab[kk][i][m0 / 4] = make_uint2(lo[i] ^ 0x80808080u, hi[i] ^ 0x80808080u);
+#pragma unroll
+            for (int c = 0; c < EPT / 4; ++c) ftab[kk][i][m0 / 4 + c] = dw[i][c] ^ 0x80808080u;
     }
     // this lane's A quarter: row r, k = 16 wv + 4 sub + e
     const int ar_r = lane & 15, ar_s = lane >> 4;
@@ -1128,9 +1134,9 @@ __device__ __forceinline__ void dec_mm_impl(const ModGemmArgs& a, uint32_t Ppad,
     uint64_t an[RS][4], bv[RS][4];
     {
         uint64_t av[4];
-        ld4(a_ptr(15), av);
+        ld4(a_ptr(KW - 1), av);
 #pragma unroll
-        for (int k = 1; k <= AH; ++k) ld4(a_ptr(15 - k), an[k % RS]);
+        for (int k = 1; k <= AH; ++k) ld4(a_ptr(KW - 1 - k), an[k % RS]);
         a_store(0, av);
     }
     // output lane: column x = 16 wv + (lane & 15), rows y = 16 yg + 4 (lane >> 4) + rr
@@ -1146,16 +1152,16 @@ __device__ __forceinline__ void dec_mm_impl(const ModGemmArgs& a, uint32_t Ppad,
         for (int rr = 0; rr < 4; ++rr) d[rr] = bp[rr * N];
     };
 #pragma unroll
-    for (int k = 0; k < AH; ++k) b_load(15 - k, bv[k % RS]);
+    for (int k = 0; k < AH; ++k) b_load(KW - 1 - k, bv[k % RS]);
 #pragma unroll
     for (int rr = 0; rr < 4; ++rr) h1[rr] = h2[rr] = t0[rr] = 0.0;
     __syncthreads();
-    // four blocks of four w: a dword of digit bytes per (row, plane) completes in each block
+    // blocks of four w: a dword of digit bytes per (row, plane) completes in each block
 #pragma unroll 1
-    for (int blk = 0; blk < 4; ++blk) {
+    for (int blk = 0; blk < KW / 4; ++blk) {
 #pragma unroll
     for (int i4 = 0; i4 < 4; ++i4) {
-        const int it = 4 * blk + i4, kk = 15 - it, buf = i4 & 1;
+        const int it = 4 * blk + i4, kk = KW - 1 - it, buf = i4 & 1;
         v4i af[D];
 #pragma unroll
         for (int i = 0; i < D; ++i) af[i] = *(const v4i*)&atab[buf][i][lane & 15][4 * (lane >> 4)];
@@ -1176,7 +1182,7 @@ __device__ __forceinline__ void dec_mm_impl(const ModGemmArgs& a, uint32_t Ppad,
 #if MFHE_DMM_SCHED
         __builtin_amdgcn_sched_barrier(0);   // the epilogue's FP64 chains stay after the MFMAs (register pressure)
 #endif
-        if (it < 15) a_store(buf ^ 1, an[(i4 + 1) % RS]);
+        if (it < KW - 1) a_store(buf ^ 1, an[(i4 + 1) % RS]);
 #pragma unroll
         for (int rr = 0; rr < 4; ++rr) {
             double z[NZ];
@@ -1207,8 +1213,8 @@ __device__ __forceinline__ void dec_mm_impl(const ModGemmArgs& a, uint32_t Ppad,
             }
         }
         // the next loads into the slots just consumed: in flight across the next AH barriers
-        if (it + 1 + AH <= 15) ld4(a_ptr(kk - 1 - AH), an[(i4 + 1 + AH) % RS]);
-        if (it + AH <= 15) b_load(kk - AH, bv[(i4 + AH) % RS]);
+        if (it + 1 + AH <= KW - 1) ld4(a_ptr(kk - 1 - AH), an[(i4 + 1 + AH) % RS]);
+        if (it + AH <= KW - 1) b_load(kk - AH, bv[(i4 + AH) % RS]);
         barrier();   // the A tile just written is read next; the one read here is rewritten after
     }
     }
@@ -1216,49 +1222,67 @@ __device__ __forceinline__ void dec_mm_impl(const ModGemmArgs& a, uint32_t Ppad,
     __syncthreads();
     {
         int8_t* const bdl = a.Bdig + ((uint64_t)l * D * (FK / 32) + kc) * (uint64_t)Ppad * 64 + (2 * ap + hf) * 16 +
-                            (uint64_t)(16 * yg * N) * 64;
+                            half * 8 + (uint64_t)(16 * yg * N) * 64;
 #pragma unroll
         for (int i = 0; i < D; ++i) {
             if (i >= nd) break;
 #pragma unroll
             for (int c4 = 0; c4 < 4; ++c4) {
                 const int cl = c4 * 256 + t;
-                *(v4i*)(bdl + (uint64_t)i * (FK / 32) * Ppad * 64 + (uint64_t)cl * 64) = *(const v4i*)dstage[i][cl];
+                int8_t* o = bdl + (uint64_t)i * (FK / 32) * Ppad * 64 + (uint64_t)cl * 64;
+                if constexpr (KW == 16) *(v4i*)o = *(const v4i*)dstage[i][cl];
+                else *(uint2*)o = *(const uint2*)dstage[i][cl];
             }
         }
     }
     const cdp_t zp = izl + 16;
     const int ch = 2 * kc + hf;   // the chunk of 16 k: its power of x1 / x2 (as k0 >> 4 in the digitize above)
+    double z1 = zp[ch], z2 = zp[16 + ch];
+    if (KW == 8 && half) {   // the upper 8 k of the chunk: x^8 more (three exact squarings)
+        double e1 = x1, e2 = x2;
+#pragma unroll
+        for (int s = 0; s < 3; ++s) {
+            e1 = ar.mulmod(e1, e1);
+            e2 = ar.mulmod(e2, e2);
+        }
+        z1 = ar.mulmod(z1, e1);
+        z2 = ar.mulmod(z2, e2);
+    }
+    const int share = ch * (16 / KW) + half;
 #pragma unroll
     for (int rr = 0; rr < 4; ++rr) {
         const uint32_t p = (uint32_t)(oy + rr) * N + ox;
-        double* po = a.dpart + (((uint64_t)ch * L + l) * Ppad + p) * 6 + ap * 3;
+        double* po = a.dpart + (((uint64_t)share * L + l) * Ppad + p) * 6 + ap * 3;
         po[0] = ar.reduce(t0[rr]);
-        po[1] = ar.reduce(ar.mulmod(h1[rr], zp[ch]));
-        po[2] = ar.reduce(ar.mulmod(h2[rr], zp[16 + ch]));
+        po[1] = ar.reduce(ar.mulmod(h1[rr], z1));
+        po[2] = ar.reduce(ar.mulmod(h2[rr], z2));
     }
 }
-// block b -> (limb, panel, row group, quarter): the four quarters of one (l, kc, yg) get ids 8 apart (one XCD)
+// block b -> (limb, panel, row group, sub): the NSUB workgroups (a', hf[, half]) of one (l, kc, yg) get ids 8 apart (one
+// XCD: its L2 merges their parts of each 64-byte group)
+constexpr int DMM_NSUB = 4 * 16 / DMM_KW;
 struct DecMmBlock {
-    int lz, kc, yg, ap, hf;
+    int lz, kc, yg, ap, hf, half;
 };
 __device__ __forceinline__ DecMmBlock dec_mm_block() {
-    const uint32_t b = blockIdx.x, j = b >> 3, g = (j >> 2) * 8 + (b & 7), qd = j & 3;
-    return DecMmBlock{(int)(g >> 5), (int)((g >> 2) & 7), (int)(g & 3), (int)(qd >> 1), (int)(qd & 1)};
+    const uint32_t b = blockIdx.x, j = b >> 3, g = (j / DMM_NSUB) * 8 + (b & 7), sb = j % DMM_NSUB;
+    const uint32_t qd = DMM_KW == 16 ? sb : sb >> 1;
+    return DecMmBlock{(int)(g >> 5), (int)((g >> 2) & 7), (int)(g & 3), (int)(qd >> 1), (int)(qd & 1),
+                      DMM_KW == 16 ? 0 : (int)(sb & 1)};
 }
 template <int D>
 __global__ __launch_bounds__(256, MFHE_DMM_WG_CU) void dec_mm_digitize_kernel(ModGemmArgs a, uint32_t Ppad, PlaneCounts pc, int L) {
     const DecMmBlock k = dec_mm_block();
-    dec_mm_impl<D>(a, Ppad, pc, k.lz, L, k.kc, k.ap, k.hf, k.yg);
+    dec_mm_impl<D>(a, Ppad, pc, k.lz, L, k.kc, k.ap, k.hf, k.yg, k.half);
 }
 template <int D>
 __global__ __launch_bounds__(256, MFHE_DMM_WG_CU) void dec_mm_digitize_pair_kernel(ModGemmArgs a, ModGemmArgs b, uint32_t Ppad,
                                                                       PlaneCounts pc, int L) {
     const DecMmBlock k = dec_mm_block();
     const bool hi = k.lz >= L;
-    dec_mm_impl<D>(hi ? b : a, Ppad, pc, hi ? k.lz - L : k.lz, L, k.kc, k.ap, k.hf, k.yg);
+    dec_mm_impl<D>(hi ? b : a, Ppad, pc, hi ? k.lz - L : k.lz, L, k.kc, k.ap, k.hf, k.yg, k.half);
 }
-constexpr int DMM_G = 16;   // column-sum shares of dec_mm_digitize_kernel: one per (kc, hf)
+constexpr int DMM_G = 16 * 16 / DMM_KW;   // column-sum shares of dec_mm_digitize_kernel: one per (kc, hf[, half])
 
 // C = sum_s acc_s * 256^s mod q for the 32 x 32 wave tile at (m0, p0) of limb l (lane = (r, h)).
 // MODE 1 (factored forward): column p0 + r is (a', p) = divmod(., Ppad), output row a' * 256 + row, plus d0.
@@ -1826,7 +1850,7 @@ static int launch_factored_inv(const ModGemmArgs& a, int L, hipStream_t s) {
         const int G = a.dskc ? DMM_G : GS;
         f.dpart = f.cc + (size_t)L * Ppad * 2;
         if (a.dskc) {
-            const dim3 gm(128 * L);
+            const dim3 gm(DMM_NSUB * 32 * L);
             if (a.D == 5) hipLaunchKernelGGL(dec_mm_digitize_kernel<5>, gm, dim3(256), 0, s, f, Ppad, pc, L);
             else hipLaunchKernelGGL(dec_mm_digitize_kernel<6>, gm, dim3(256), 0, s, f, Ppad, pc, L);
             MFHE_CHECK_LAUNCH("dec_mm_digitize_kernel");
@@ -1914,7 +1938,7 @@ int launch_mod_gemm_pair(const ModGemmArgs& a, const ModGemmArgs& b, int L, hipS
             x.dpart = x.cc + (size_t)L * Ppad * 2;
         }
         if (mm) {
-            const dim3 gm(256 * L);
+            const dim3 gm(DMM_NSUB * 64 * L);
             if (a.D == 5) hipLaunchKernelGGL(dec_mm_digitize_pair_kernel<5>, gm, dim3(256), 0, s, f[0], f[1], Ppad, pc, L);
             else hipLaunchKernelGGL(dec_mm_digitize_pair_kernel<6>, gm, dim3(256), 0, s, f[0], f[1], Ppad, pc, L);
             MFHE_CHECK_LAUNCH("dec_mm_digitize_pair_kernel");

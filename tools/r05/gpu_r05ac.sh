@@ -6,8 +6,13 @@ LP=$ROOT/matrix-fhe-gpu_amd
 timeout -k 10 200 python -u -m pytest tests/test_he_gpu.py -x -q -k "dec_mm or fused_ring" --timeout 120 --timeout-method thread \
     > $O/pytest_mm.log 2>&1 || { tail -40 $O/pytest_mm.log; exit 1; }
 tail -1 $O/pytest_mm.log
+for v in k8 k8a1; do
+  MFHE_LIB=$LP/libmfhe_$v.so timeout -k 10 200 python -u -m pytest tests/test_he_gpu.py -x -q -k "dec_mm" --timeout 120 \
+      --timeout-method thread > $O/pytest_$v.log 2>&1 || { tail -40 $O/pytest_$v.log; exit 1; }
+  echo "$v: $(tail -1 $O/pytest_$v.log)"
+done
 cd /tmp && export TMPDIR=/tmp
-for v in base; do
+for v in base k8 k8a1; do
   case $v in base) lib=$LP/libmfhe.so;; *) lib=$LP/libmfhe_$v.so;; esac
   MFHE_DEC_MM=1 MFHE_LIB=$lib timeout -k 10 200 rocprofv3 --kernel-trace --stats -d "$O/prof_$v" -o run --output-format csv -- \
       python3 "$ROOT/tools/pipeline_bench.py" 10 > "$O/prof_$v.log" 2>&1 || { echo "prof failed"; tail -5 $O/prof_$v.log; exit 4; }
