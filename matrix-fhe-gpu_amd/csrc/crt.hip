@@ -216,6 +216,9 @@ __device__ __forceinline__ bool fast_f64_divides(int64_t c, uint64_t x, const Cr
 // as |c - x_k| * q_k^-1 mod 2^64 <= floor((2^64-1)/q_k) (q_k odd); by CRT uniqueness c is then THE
 // centred value, bit-identical to compose_slow.  Residues are loaded CH limbs at a time so each thread
 // has CH loads in flight; for L <= CH the divisibility pass reuses the registers.
+#ifndef MFHE_CRT_NT
+#define MFHE_CRT_NT 1   // the fast compose's residue loads nontemporal (read once; 0 for A/B)
+#endif
 template <int CH>
 __device__ __forceinline__ bool compose_fast_f64(const uint64_t* __restrict__ in, uint64_t ncoeff, int L, int Lg,
                                                  uint64_t shard_stride, const CrtLimbF* __restrict__ lf,
@@ -229,7 +232,7 @@ __device__ __forceinline__ bool compose_fast_f64(const uint64_t* __restrict__ in
 #pragma unroll
         for (int i = 0; i < CH; ++i) {
             if (k0 + i < L) {
-                xs[i] = p[(uint64_t)j * ncoeff];
+                xs[i] = MFHE_CRT_NT ? __builtin_nontemporal_load(p + (uint64_t)j * ncoeff) : p[(uint64_t)j * ncoeff];
                 if (++j == Lg) {
                     j = 0;
                     p += shard_stride;

@@ -15,6 +15,9 @@
 #ifndef MFHE_DEC_SUBS
 #define MFHE_DEC_SUBS 4   // decrypt-fused digitize: 16-row substeps loaded together (1, 2 or 4)
 #endif
+#ifndef MFHE_DEC_NT
+#define MFHE_DEC_NT 1   // decrypt-fused digitize: the ciphertext loads nontemporal (read once; 0 for A/B)
+#endif
 #ifndef MFHE_DEC_SPLIT
 #define MFHE_DEC_SPLIT 4   // decrypt-fused digitize: workgroups per (row, limb), each 8 / MFHE_DEC_SPLIT panels
 #endif
@@ -868,9 +871,9 @@ __device__ __forceinline__ void ifold_dec_impl(const ModGemmArgs& a, uint32_t Pp
             const int rr = st * 16 + rs;
             const uint64_t w = (uint64_t)(rr >> 5) * FK + kc * 32 + (rr & 31);
             const uint64_t wl = w * L + l, r0 = (wl * N + y) * N;
-            ld4(a.dct + a.dtotal + r0 + 4 * j, av[si]);
+            ld4<MFHE_DEC_NT>(a.dct + a.dtotal + r0 + 4 * j, av[si]);
             ld4(a.dsk + wl * N + 4 * j, sk[si]);
-            ld4(a.dct + r0 + 4 * j, bv[si]);
+            ld4<MFHE_DEC_NT>(a.dct + r0 + 4 * j, bv[si]);
         }
         // ring product per row (the shuffle ring_mul_row: ring_mul_row64_lds measured slower here, 198 vs 183 us)
 #pragma unroll

@@ -198,6 +198,9 @@ struct RingArgs {
     uint64_t rows;           // 512 n L
 };
 
+#ifndef MFHE_ENC_NT
+#define MFHE_ENC_NT 1   // enc_ring_kernel's row streams as nontemporal accesses (read / written once; 0 for A/B)
+#endif
 // encrypt, fused: t = a * s over X (ring_mul_row), then encrypt_pair's combine (HE.cu:1530-1552):
 // ct_k.b = m_k - t + e, ct_k.a = a, written matrix-major; a, e poly-major.  One thread: 4 coefficients
 // of matrix row R = (w L + l) n + y.
@@ -221,14 +224,15 @@ __global__ __launch_bounds__(256) void enc_ring_kernel(RingArgs ra, const uint64
     const LimbConst lc = ra.lf[l];
     const ArithF64 ar(lc);
     uint64_t av[4], sk[4];
-    ld_row<LDS>(aev + (a_mm ? i0 : p0), j, av);
+    constexpr bool NT = MFHE_ENC_NT && LDS;
+    ld_row<LDS, NT>(aev + (a_mm ? i0 : p0), j, av);
     ld4(ra.sk + ((uint64_t)w * ra.L + l) * N + 4 * j, sk);
     // the combine's operands are loaded before the ring product (clamped rows for dead lanes), so their latency
     // overlaps the butterflies instead of following them
     uint64_t ev[4], mv[4], mi[4], b[4];
-    ld_row<LDS>(e + p0, j, ev);
-    ld_row<LDS>(m_re + i0, j, mv);
-    if (m_im) ld_row<LDS>(m_im + i0, j, mi);
+    ld_row<LDS, NT>(e + p0, j, ev);
+    ld_row<LDS, NT>(m_re + i0, j, mv);
+    if (m_im) ld_row<LDS, NT>(m_im + i0, j, mi);
     double x[4], sv[4];
 #pragma unroll
     for (int s = 0; s < 4; ++s) {
@@ -251,13 +255,13 @@ __global__ __launch_bounds__(256) void enc_ring_kernel(RingArgs ra, const uint64
     };
 #pragma unroll
     for (int s = 0; s < 4; ++s) b[s] = bval(mv[s], s);
-    st_row<LDS>(ct_re + i0, j, b);
-    if (!a_mm) st_row<LDS>(ct_re + total + i0, j, av);
+    st_row<LDS, NT>(ct_re + i0, j, b);
+    if (!a_mm) st_row<LDS, NT>(ct_re + total + i0, j, av);
     if (m_im) {
 #pragma unroll
         for (int s = 0; s < 4; ++s) b[s] = bval(mi[s], s);
-        st_row<LDS>(ct_im + i0, j, b);
-        if (!a_mm) st_row<LDS>(ct_im + total + i0, j, av);
+        st_row<LDS, NT>(ct_im + i0, j, b);
+        if (!a_mm) st_row<LDS, NT>(ct_im + total + i0, j, av);
     }
 }
 

@@ -182,9 +182,16 @@ __device__ __forceinline__ void ring_mul_row64_lds(double (&x)[4], const double 
 }
 
 // 4 consecutive u64 (32-byte aligned) as two 16-byte accesses
+template <bool NT = false>
 __device__ __forceinline__ void ld4(const uint64_t* p, uint64_t (&v)[4]) {
-    const ulonglong2 a = *(const ulonglong2*)p, b = *(const ulonglong2*)(p + 2);
-    v[0] = a.x; v[1] = a.y; v[2] = b.x; v[3] = b.y;
+    if constexpr (NT) {
+        typedef unsigned long long u64x2 __attribute__((ext_vector_type(2)));
+        const u64x2 a = __builtin_nontemporal_load((const u64x2*)p), b = __builtin_nontemporal_load((const u64x2*)(p + 2));
+        v[0] = a.x; v[1] = a.y; v[2] = b.x; v[3] = b.y;
+    } else {
+        const ulonglong2 a = *(const ulonglong2*)p, b = *(const ulonglong2*)(p + 2);
+        v[0] = a.x; v[1] = a.y; v[2] = b.x; v[3] = b.y;
+    }
 }
 __device__ __forceinline__ void st4(uint64_t* p, const uint64_t (&v)[4]) {
     *(ulonglong2*)p = make_ulonglong2(v[0], v[1]);
@@ -193,20 +200,24 @@ __device__ __forceinline__ void st4(uint64_t* p, const uint64_t (&v)[4]) {
 
 // lane j's four coefficients of a row starting at p: 4 j .. 4 j + 3 (ring_mul_row), or j + 16 s (ring_mul_row64_lds,
 // A = true: four 8-byte accesses, each a 128-byte sweep over the row's 16 lanes)
-template <bool A>
+// NT: nontemporal (streamed once, no reuse: MFHE_ENC_NT)
+template <bool A, bool NT = false>
 __device__ __forceinline__ void ld_row(const uint64_t* p, int j, uint64_t (&v)[4]) {
     if constexpr (A) {
 #pragma unroll
-        for (int s = 0; s < 4; ++s) v[s] = p[j + 16 * s];
+        for (int s = 0; s < 4; ++s) v[s] = NT ? __builtin_nontemporal_load(p + j + 16 * s) : p[j + 16 * s];
     } else {
         ld4(p + 4 * j, v);
     }
 }
-template <bool A>
+template <bool A, bool NT = false>
 __device__ __forceinline__ void st_row(uint64_t* p, int j, const uint64_t (&v)[4]) {
     if constexpr (A) {
 #pragma unroll
-        for (int s = 0; s < 4; ++s) p[j + 16 * s] = v[s];
+        for (int s = 0; s < 4; ++s) {
+            if constexpr (NT) __builtin_nontemporal_store(v[s], p + j + 16 * s);
+            else p[j + 16 * s] = v[s];
+        }
     } else {
         st4(p + 4 * j, v);
     }
