@@ -198,10 +198,16 @@ struct ArithU64 {
 // pinned to VGPRs here (ArithU64(c, false)): pinned, the column pass spilled at its 128-VGPR bound and fell back.
 struct ArithU60 : ArithU64 {
     uint64_t n8q;
-    float qs;   // 2^32 / q (1 - 2^-20), canon's quotient scale
+    uint32_t sh;   // canon's window: x >> sh < 2^32 for x < 16q (sh = max(0, bitlen(q) - 28))
+    float qs;      // 2^sh / q (1 - 2^-20), canon's quotient scale
 
+    __device__ __forceinline__ static uint32_t window(uint64_t q) {
+        const int b = 64 - __clzll((long long)q);
+        return b > 28 ? (uint32_t)(b - 28) : 0u;
+    }
     __device__ __forceinline__ explicit ArithU60(const LimbConst& c)
-        : ArithU64(c, false), n8q(0 - 8 * c.q), qs((float)(c.qinv * (4294967296.0 * (1.0 - 0x1p-20)))) {}
+        : ArithU64(c, false), n8q(0 - 8 * c.q), sh(window(c.q)),
+          qs((float)(c.qinv * (double)(1ull << window(c.q)) * (1.0 - 0x1p-20))) {}
     __device__ __forceinline__ uint64_t mulmod(uint64_t v, Tw w) const {
         const uint64_t Q = mulhi64(v, w.y);
         const uint32_t vl = (uint32_t)v, vh = (uint32_t)(v >> 32), wl = (uint32_t)w.x, wh = (uint32_t)(w.x >> 32);
@@ -225,13 +231,18 @@ struct ArithU60 : ArithU64 {
     }
     __device__ __forceinline__ uint64_t round_reduce(uint64_t x) const { return x; }
     __device__ __forceinline__ uint64_t raw_out(uint64_t x) const { return x; }
-    // [0, 16q) -> [0, q): the quotient k = floor(x / q) - {0, 1} from the high word in FP32 (x / q < 16, so the
-    // high word's truncation and two FP32 roundings are far below 1; the scale is shaded down by 2^-20 so k never
-    // exceeds the quotient), x - k q in [0, 2q) by one mad, then one select: 10 VALU instructions instead of four
-    // selects' 20
+    // [0, 16q) -> [0, q): the quotient k = floor(x / q) - {0, 1} from a 32-bit window of x in FP32, x - k q in
+    // [0, 2q) by one mad, then one select: 11 VALU instructions instead of four selects' 20.  The window
+    // xs = x >> sh with sh = max(0, bitlen(q) - 28) holds all of x's significant bits down to 2^-27 q
+    // (x < 16q < 2^(bitlen(q) + 4)), so with b = bitlen(q):
+    //   x/q - xs 2^sh / q < 2^sh / q <= 2^-27,  three FP32 roundings <= 3 * 2^-24 relative,
+    // and the scale, shaded down by 2^-20 relative (> the roundings), keeps k <= floor(x / q) while the total
+    // shortfall 16 (2^-20 + 3 * 2^-24) + 2^-27 < 2e-5 keeps k >= floor(x / q) - 1, for every q < 2^60.
+    // (r05 took the window as the high word for every q; for q < 2^33 the dropped low word is worth >= 0.5 of a
+    // quotient step and canon returned residues >= q: tests/test_ntt_gpu.py modulus-size sweep)
     __device__ __forceinline__ uint64_t canon(uint64_t x) const {
         float f;
-        asm("v_cvt_f32_u32 %0, %1" : "=v"(f) : "v"((uint32_t)(x >> 32)));
+        asm("v_cvt_f32_u32 %0, %1" : "=v"(f) : "v"((uint32_t)(x >> sh)));
         uint32_t k;
         asm("v_cvt_u32_f32 %0, %1" : "=v"(k) : "v"(f * qs));
         uint64_t r, c;

@@ -57,10 +57,11 @@ def _kernel_asm(symbol_re: str) -> str:
     pytest.fail(f"kernel {symbol_re} not found in {LIB}")
 
 
-@pytest.mark.parametrize("arith", ["F64", "U64"])
-@pytest.mark.parametrize("inv", [False, True], ids=["forward-first-pass", "inverse-last-pass"])
+@pytest.mark.parametrize("arith,inv", [("F64", False), ("F64", True), ("U64", False), ("U64", True), ("U60", False)],
+                         ids=["F64-forward-first-pass", "F64-inverse-last-pass", "U64-forward-first-pass",
+                              "U64-inverse-last-pass", "U60-forward-first-pass"])
 def test_column_pass_dma_waits_match_the_instruction_mix(inv, arith):
-    sb = arith == "U64"   # the U64 column pass runs the single-buffer form (ntt_plans.hpp col_db_single)
+    sb = arith != "F64"   # the U64 / U60 column pass runs the single-buffer form (ntt_plans.hpp col_db_single)
     asm = _kernel_asm(r"_ZN4mfhe17ntt_col_db_kernelINS_8Arith" + arith + r"ENS_6TwSrc" + arith[0] +
                       r"ELb" + ("1" if inv else "0") + r"ELb" + ("1" if sb else "0") + r"E[^>]*")
     ops = collections.Counter(re.findall(r"^\s+((?:global|buffer|flat|scratch)_[a-z0-9_]+)", asm, re.M))
@@ -69,7 +70,7 @@ def test_column_pass_dma_waits_match_the_instruction_mix(inv, arith):
     # intermediate (plain global stores), the inverse's output (sc1 nt buffer stores)
     store = "buffer_store_dwordx2" if inv else "global_store_dwordx2"
     # U64: + 1 DMA instruction per wave for the limb's twiddle table (issued before the limb's vmcnt(0))
-    assert ops["global_load_lds_dwordx4"] == (17 if arith == "U64" else 16), ops
+    assert ops["global_load_lds_dwordx4"] == (17 if sb else 16), ops
     assert ops[store] == 16, ops
     assert not any(k.startswith("scratch_") for k in ops), ops            # no spills
     assert not any("store" in k for k in ops if k != store), ops
