@@ -607,7 +607,6 @@ extern "C" int mfhe_ctx_create(const uint64_t* moduli, int L, int log_n, int con
 extern "C" int mfhe_ctx_destroy(mfhe_ctx* c) {
     if (!c) return MFHE_OK;
     if (c->ws) (void)hipFree(c->ws);
-    if (c->d_xl2) (void)hipFree(c->d_xl2);
     if (c->gemm_ws) (void)hipFree(c->gemm_ws);
     if (c->gemm_ws2) (void)hipFree(c->gemm_ws2);
     if (c->he_side) (void)hipStreamDestroy(c->he_side);
@@ -659,7 +658,9 @@ extern "C" int mfhe_ctx_set_option(mfhe_ctx* c, int opt, int64_t v) {
             c->ntt_chunk_bytes = v;
             return MFHE_OK;
         case MFHE_OPT_NTT_PLAN:
-            if (v < 0 || v > 5 || v == 4) return set_error(MFHE_EINVAL, "plan must be 0, 1, 2, 3 or 5");
+            // 5 (the one-launch N = 2^16 forward with an in-L2 hand-off, r05) was removed in r06: latency-bound at the one
+            // wave per SIMD its LDS allows and slower than the two passes (profiles/r06_xl2_sq_pmc.txt)
+            if (v < 0 || v > 3) return set_error(MFHE_EINVAL, "plan must be 0, 1, 2 or 3");
             c->ntt_plan = (int)v;
             return MFHE_OK;
         case MFHE_OPT_NTT_WG_PER_CU:
@@ -747,12 +748,6 @@ extern "C" int mfhe_ctx_get_option(const mfhe_ctx* c, int opt, int64_t* v) {
     switch (opt) {
         case MFHE_OPT_NTT_CHUNK_BYTES: *v = c->ntt_chunk_bytes; return MFHE_OK;
         case MFHE_OPT_NTT_PLAN: *v = c->ntt_plan; return MFHE_OK;
-        case MFHE_OPT_NTT_XL2_TIMEOUT: {   // synchronous read of the plan-5 kernel's sticky timeout word (tests)
-            uint32_t w = 0;
-            if (c->d_xl2) MFHE_HIP(hipMemcpy(&w, c->d_xl2 + 513, sizeof w, hipMemcpyDeviceToHost));
-            *v = w;
-            return MFHE_OK;
-        }
         case MFHE_OPT_NTT_PLAN_EFFECTIVE:
             *v = mfhe::ntt_phantom_plan(c->arith == MFHE_ARITH_F64, c->logN, c->ntt_plan, true);
             return MFHE_OK;

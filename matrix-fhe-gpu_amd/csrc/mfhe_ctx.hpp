@@ -69,12 +69,8 @@ struct NttTablesU {   // U64 path / phantom format
 namespace mfhe {
 // The launch plan a phantom NTT call runs (MFHE_OPT_NTT_PLAN_EFFECTIVE; ntt_plans.hpp run_phantom follows it):
 // 4 = the pipelined single pass (N = 2^14, FP64, context limb table), 1 = one pass per polynomial (plain), 2 = two
-// passes, 5 = the one-launch XCD-L2 hand-off (N = 2^16, FP64, forward; ntt_xl2.hpp).  plan: MFHE_OPT_NTT_PLAN (0 / 3 auto, 1 single, 2 two passes from log_n 12).
+// passes.  plan: MFHE_OPT_NTT_PLAN (0 / 3 auto, 1 single, 2 two passes from log_n 12).
 inline int ntt_phantom_plan(bool f64, int logN, int plan, bool limbs) {
-    if (plan == 5) {   // the one-launch N = 2^16 FP64 forward; every other shape (and the inverse) as auto
-        if (f64 && logN == 16 && limbs) return 5;
-        plan = 0;
-    }
     const bool autoplan = plan == 0 || plan == 3;
     if (f64 && logN == 14 && limbs && autoplan) return 4;
     const bool two = logN > 14 || (plan == 2 && logN >= 12) || (autoplan && logN == 14);
@@ -178,9 +174,6 @@ struct mfhe_ctx {
 
     int trace_split = 2;              // MFHE_OPT_TRACE_SPLIT: split-digit kernel (2 MFMA, 1 VALU) when every q < 2^45
 
-    // N = 2^16 one-launch NTT (MFHE_OPT_NTT_PLAN 5, ntt_xl2.hpp): queue / counter state, grown on demand
-    uint32_t* d_xl2 = nullptr;
-    size_t xl2_words = 0;
 
     // pipeline workspace (allocated on first use / mfhe_ctx_reserve_workspace)
     void* ws = nullptr;

@@ -119,7 +119,7 @@ __device__ __forceinline__ void coldb_tile(uint64_t* buf, uint32_t gl, uint32_t 
     for (int k = 0; k < C::R; ++k) {
         const uint64_t o = ar.raw_out(x[k]);
         if constexpr (STORE) base[off0 | ((uint32_t)Gm::g_of(1, tau, k) << logS)] = o;
-        else asm volatile("" ::"v"(o));   // timing probe (ntt_xl2.hpp MFHE_XL2_PROBE): no store
+        else asm volatile("" ::"v"(o));   // timing probe (no store)
     }
 }
 

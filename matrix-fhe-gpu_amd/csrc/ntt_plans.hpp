@@ -14,7 +14,6 @@
 #include "mfhe_ctx.hpp"
 #include "ntt_coldb.hpp"
 #include "ntt_single14.hpp"
-#include "ntt_xl2.hpp"
 
 // Groups (contiguous rows) per block-pass workgroup.  N = 2^16: 4 rows (64 threads, 8.7 KiB LDS) rather than 16
 // (256 threads, 34.9 KiB): the block pass gains from residency and 16-row tiles are LDS-bound at 4 per CU;
@@ -311,44 +310,6 @@ static int two_pass(const NttJob<TS>& j, hipStream_t st) {
     return MFHE_OK;
 }
 
-// N = 2^16 forward in one launch (ntt_xl2.hpp, MFHE_OPT_NTT_PLAN 5).  Host side: ctx-owned state (grown on demand, zeroed on the stream before every launch), one persistent
-// launch over the whole batch.  j.ctx and the limb table are required (the caller falls back otherwise).
-template <class TS>
-static int launch_xl2(const NttJob<TS>& j, hipStream_t st) {
-    constexpr uint32_t M = MFHE_XL2_M, LAM = MFHE_XL2_LAM;
-    static_assert(LAM >= 1, "the deferred A signals need the B blocks one chunk behind");
-    const uint64_t npl = j.batch * (uint64_t)j.nl;
-    if (npl == 0) return MFHE_OK;
-    if (npl >= 0x7FFFFFFFull) return set_error(MFHE_EINVAL, "NTT batch too large for one launch");
-    mfhe_ctx* c = j.ctx;
-    Xl2Args a{};
-    a.data = j.data;
-    a.tw = j.tw.p;
-    a.limbs = j.limbs;
-    a.batch = (uint32_t)j.batch;
-    a.nl = (uint32_t)j.nl;
-    a.start_limb = (uint32_t)j.start_limb;
-    a.npoly = (uint32_t)npl;
-    a.nchunk = (uint32_t)((npl + M - 1) / M);
-    a.cmax = a.nchunk;   // an XCD's chunks: at most all of them (one XCD present)
-    const size_t words = xl2_state_words(a.cmax);
-    if (c->xl2_words < words) {
-        if (c->d_xl2) MFHE_HIP(hipFree(c->d_xl2));
-        c->d_xl2 = nullptr;
-        c->xl2_words = 0;
-        MFHE_HIP(hipMalloc(&c->d_xl2, words * sizeof(uint32_t)));
-        c->xl2_words = words;
-    }
-    a.st = c->d_xl2;
-    MFHE_HIP(hipMemsetAsync(a.st, 0, words * sizeof(uint32_t), st));
-    const size_t lds = 2 * ((size_t)ColDb::BUF + 4096) * sizeof(uint64_t);   // two slots: tile + B twiddles
-    const uint32_t grid = (uint32_t)(j.num_cus * MFHE_XL2_WPC);
-    constexpr int LOG_R = MFHE_XL2_LOG_R;
-    hipLaunchKernelGGL((ntt16_xl2_kernel<M, LAM, LOG_R>), dim3(grid), dim3(Xl2G<LOG_R>::NT), lds, st, a);
-    MFHE_CHECK_LAUNCH("ntt16_xl2_kernel launch");
-    return MFHE_OK;
-}
-
 template <class A, class TS, bool INV>
 static int run_phantom(const NttJob<TS>& j, hipStream_t st) {
     // auto (plan 0, or 3): N = 2^14 with FP64 arithmetic and the context's limb table runs the pipelined single pass
@@ -359,11 +320,7 @@ static int run_phantom(const NttJob<TS>& j, hipStream_t st) {
     int kind = ntt_phantom_plan(std::is_same<A, ArithF64>::value, j.logN, j.plan, j.limbs != nullptr);
     if constexpr (std::is_same<A, ArithF64>::value) {
         if (kind == 4) return launch_s14<INV>(j, st);
-        if constexpr (!INV) {
-            if (kind == 5 && j.ctx) return launch_xl2(j, st);
-        }
     }
-    if (kind == 5) kind = ntt_phantom_plan(std::is_same<A, ArithF64>::value, j.logN, 0, j.limbs != nullptr);   // inverse
     const bool two = kind == 2;
     if (!two) return run_single<A, TS, INV, false>(j, st);
     switch (j.logN) {

@@ -61,7 +61,7 @@ def _check(got, want, what):
                         f"vs {F.top_digest(want)})"
 
 
-def _run_ntt_config(mfhe, orc, dig, name, arith=0, prefetch=None, plan=None):
+def _run_ntt_config(mfhe, orc, dig, name, arith=0, prefetch=None):
     import torch
     cfg = F.NTT_CONFIGS[name]
     N = 1 << cfg["log_n"]
@@ -72,8 +72,6 @@ def _run_ntt_config(mfhe, orc, dig, name, arith=0, prefetch=None, plan=None):
         ctx.set_arith(arith)
     if prefetch is not None:   # default 2: the DMA column pass; 0: the plain column pass
         ctx.set_option(mfhe.OPT_NTT_PREFETCH, prefetch)
-    if plan is not None:       # 5: the one-launch N = 2^16 forward (ntt_xl2.hpp)
-        ctx.set_option(mfhe.OPT_NTT_PLAN, plan)
     B, nl, st = cfg["batch"], cfg["nl"], cfg["start"]
     per = nl * N
     step = F.CHUNK_POLYS[cfg["log_n"]]
@@ -99,12 +97,6 @@ def test_c2_full_shape(mfhe, orc, dig):
                          ids=["f64", "u64", "f64-plain-colpass", "u64-plain-colpass"])
 def test_c3_full_shape(mfhe, orc, dig, arith, prefetch):
     _run_ntt_config(mfhe, orc, dig, "c3", arith, prefetch)
-
-
-def test_c3_full_shape_one_launch_xl2(mfhe, orc, dig):
-    """C3 through MFHE_OPT_NTT_PLAN 5 (the forward in one launch with the column -> block hand-off in each XCD's L2)
-    against the oracle's digests of all 8192 transforms."""
-    _run_ntt_config(mfhe, orc, dig, "c3", plan=5)
 
 
 def test_c3_60bit_primes_full_shape(mfhe, orc, dig):

@@ -455,70 +455,18 @@ def test_column_pass_dma_prefetch_matches_oracle(mfhe, orc, log_n, batch, nl):
         np.testing.assert_array_equal(mfhe.to_host_u64(d), data)
 
 
-@pytest.mark.parametrize("batch,nl,start", [(1, 1, 0), (1, 3, 2), (5, 3, 1), (33, 2, 0), (64, 8, 0)])
-def test_xl2_one_launch_matches_oracle_and_two_pass(mfhe, orc, batch, nl, start):
-    """MFHE_OPT_NTT_PLAN 5 (ntt_xl2.hpp): the N = 2^16 forward in one launch, column -> block hand-off in each XCD's
-    L2 -- bit-exact against the oracle (small batches) and against the two-pass plan, for a single polynomial
-    (most XCDs get nothing), odd counts (a partial last mini-chunk), limb sub-ranges and limb changes inside the
-    launch; all-(q - 1) first polynomial; no bounded spin may time out; the inverse under plan 5 runs auto."""
-    import torch
-    log_n, N = 16, 1 << 16
-    moduli = orc.gen_primes(50, 4 * N, start + nl)
-    ctx = mfhe.Context(moduli, log_n)
-    sub = moduli[start:start + nl]
-    data = rand_residues(np.random.default_rng(batch * 31 + nl), batch, sub, N)
-    data[:nl * N] = (np.array(sub, np.uint64)[:, None] - np.uint64(1)).repeat(N, axis=1).ravel()
-    ctx.set_option(mfhe.OPT_NTT_PLAN, 0)
-    d = mfhe.to_device_u64(data)
-    ctx.ntt_fwd(d, batch=batch, start_limb=start, nlimbs=nl)
-    torch.cuda.synchronize()
-    want = mfhe.to_host_u64(d)
-    if batch * nl <= 15:
-        np.testing.assert_array_equal(want, orc.phantom_fwd(data, nl, log_n, sub))
-    ctx.set_option(mfhe.OPT_NTT_PLAN, 5)
-    assert ctx.get_option(mfhe.OPT_NTT_PLAN_EFFECTIVE) == 5
-    for _ in range(3):
-        d = mfhe.to_device_u64(data)
-        ctx.ntt_fwd(d, batch=batch, start_limb=start, nlimbs=nl)
-        torch.cuda.synchronize()
-        assert ctx.get_option(mfhe.OPT_NTT_XL2_TIMEOUT) == 0
-        np.testing.assert_array_equal(mfhe.to_host_u64(d), want)
-    ctx.ntt_inv(d, batch=batch, start_limb=start, nlimbs=nl)
-    torch.cuda.synchronize()
-    np.testing.assert_array_equal(mfhe.to_host_u64(d), data)
-    ctx.close()
-
-
-def test_xl2_stress_every_word_under_uneven_load(mfhe, orc):
-    """The L2 hand-off under stress (the guide's rule for in-launch hand-offs: uneven load, every word checked):
-    320 launches of plan 5 on 192 polynomials (N = 2^16, 8 limbs x 24), every output word compared with the two-pass
-    plan's; every other launch runs beside a side-stream copy kernel that takes CUs and bandwidth away from some
-    workgroups.  Any stale intermediate line would show as a wrong word."""
-    import torch
-    log_n, N, L, B = 16, 1 << 16, 8, 24
-    moduli = orc.gen_primes(50, 4 * N, L)
-    ctx = mfhe.Context(moduli, log_n)
-    data = torch.from_numpy(rand_residues(np.random.default_rng(77), B, moduli, N).view(np.int64)).cuda()
-    ref = data.clone()
-    ctx.set_option(mfhe.OPT_NTT_PLAN, 0)
-    ctx.ntt_fwd(ref, batch=B)
-    ctx.set_option(mfhe.OPT_NTT_PLAN, 5)
-    side = torch.cuda.Stream()
-    hog_a = torch.empty(64 << 20, dtype=torch.int64, device="cuda")
-    hog_b = torch.empty_like(hog_a)
-    d = torch.empty_like(data)
-    bad = 0
-    for it in range(320):
-        d.copy_(data)
-        if it & 1:
-            side.wait_stream(torch.cuda.current_stream())
-            with torch.cuda.stream(side):
-                hog_b.copy_(hog_a)
-        ctx.ntt_fwd(d, batch=B)
-        if not torch.equal(d, ref):
-            bad += 1
-        torch.cuda.current_stream().wait_stream(side)
-    torch.cuda.synchronize()
-    assert ctx.get_option(mfhe.OPT_NTT_XL2_TIMEOUT) == 0
-    assert bad == 0, f"{bad} of 320 launches had wrong words"
+def test_plan5_removed(mfhe, orc):
+    """MFHE_OPT_NTT_PLAN 5 (the one-launch N = 2^16 forward with the column -> block hand-off in each XCD's L2, r05) and
+    its timeout word MFHE_OPT_NTT_XL2_TIMEOUT (16) were removed in r06. Its SQ counters showed it latency-bound at the
+    one wave per SIMD its 132 KiB of LDS allows (profiles/r06_xl2_sq_pmc.txt), and it ran slower than the two passes.
+    Both options now fail loudly. The plans that remain are still accepted."""
+    ctx = mfhe.Context(orc.gen_primes(50, 1 << 18, 1), 16)
+    for plan in (0, 1, 2, 3):
+        ctx.set_option(mfhe.OPT_NTT_PLAN, plan)
+    for bad in (4, 5):
+        with pytest.raises(mfhe.MfheError) as e:
+            ctx.set_option(mfhe.OPT_NTT_PLAN, bad)
+        assert e.value.code == mfhe.EINVAL
+    with pytest.raises(mfhe.MfheError):
+        ctx.get_option(16)
     ctx.close()
