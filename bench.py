@@ -450,8 +450,8 @@ def c5_line(world, rank, barrier, timed, backend, reps=2, recv_gib=2.0):
         comm = mfhe.Comm.create()
         modes = ("alltoall", "allgather")
     else:
-        # N = 1: the local compose, and the same native chunked path over a 1-rank communicator (its "exchange"
-        # is a device copy), which prices the pipeline's own overhead
+        # N = 1: the local compose, and the same native chunked call over a 1-rank communicator, which exchanges
+        # nothing and composes straight from the shard (dist.cpp world-1 path): it must cost what the local compose does
         comm = mfhe.Comm.from_id(mfhe.Comm.unique_id(), 1, 0)
         modes = ("local", "alltoall")
     # chunk so one receive half holds <= recv_gib / 2 (two halves, exchange k + 1 beside compose k): all-to-all
@@ -508,17 +508,25 @@ def c5_line(world, rank, barrier, timed, backend, reps=2, recv_gib=2.0):
                   "max_err_all_rows": err, "check_2^-36": err <= 2.0 ** -36}
         if m != "local":
             res[m]["path"] = ("mfhe_crt_recombine_chunked: RCCL exchange of chunk k+1 on the communicator's stream "
-                              "beside the compose of chunk k, two receive halves" +
-                              (" (1-rank communicator: the exchange is a device copy)" if world == 1 else ""))
-            # the same chunked call with the composes skipped (MFHE_RECOMBINE_EXCHANGE_ONLY): the exchange alone,
-            # so recombine_ms against exchange_only_ms + compose_ms shows how much of the two overlaps
-            w_x, _ = timed(lambda m=m: ctx_all.crt_recombine_chunked(comm, m, shard, batch, N, chunks[m], None,
-                                                                     stream=stream, flags=mfhe.RECOMBINE_EXCHANGE_ONLY),
-                           reps, 1)
-            res[m]["exchange_only_ms"] = round(w_x / reps * 1e3, 3)
-            if "local" in res:
-                # the local compose of all 4096 polys at N = 1 (its recombine_ms); a rank composes 1/G of them
-                res[m]["compose_only_ms_est"] = round(res["local"]["recombine_ms"] / world, 3)
+                              "beside the compose of chunk k, two receive halves" if world > 1 else
+                              "mfhe_crt_recombine_chunked on a 1-rank communicator: no exchange, one compose from the shard")
+            # the recombine call alone, then the same call with the composes skipped (MFHE_RECOMBINE_EXCHANGE_ONLY) and
+            # with the exchanges skipped (MFHE_RECOMBINE_COMPOSE_ONLY: the composes out of the halves the last call
+            # filled, real values).  overlap_frac = 1 - (recombine - max(x, c)) / min(x, c): 1 when the shorter of
+            # exchange and compose hides entirely under the longer, 0 when they run back to back
+            def rec(fl=0, m=m, o=None):
+                ctx_all.crt_recombine_chunked(comm, m, shard, batch, N, chunks[m], o, stream=stream, flags=fl)
+            w_r, _ = timed(lambda: rec(o=out), reps, 1)
+            w_x, _ = timed(lambda: rec(mfhe.RECOMBINE_EXCHANGE_ONLY), reps, 1)
+            w_c, _ = timed(lambda: rec(mfhe.RECOMBINE_COMPOSE_ONLY, o=out), reps, 1)
+            r_ms, x_ms, c_ms = (w / reps * 1e3 for w in (w_r, w_x, w_c))
+            res[m]["recombine_only_ms"] = round(r_ms, 3)
+            res[m]["exchange_only_ms"] = round(x_ms, 3)
+            res[m]["compose_only_ms"] = round(c_ms, 3)
+            lo, hi = min(x_ms, c_ms), max(x_ms, c_ms)
+            res[m]["overlap_frac"] = round(1.0 - (r_ms - hi) / lo, 3) if lo > 0.01 * hi else None
+            if res[m]["overlap_frac"] is None:
+                res[m]["overlap_note"] = "no exchange to overlap (world 1)" if world == 1 else "exchange or compose ~0"
     if comm is not None:
         comm.close()
     ctx.close()
@@ -916,7 +924,8 @@ def main():
 
     # The headline is measured and complete.  The secondary lines below run collectives that have never executed
     # on more than one real GPU (RCCL communicators of libmfhe beside torch's): a watchdog on every rank bounds
-    # them, so a hang there still leaves the headline line printed (rank 0) and every rank exiting 0.
+    # them, so a hang there still leaves the headline line printed (rank 0); the stopped run then exits with
+    # WATCHDOG_EXIT (3), so the driver sees that the secondary lines did not finish.
     wd = start_watchdog(out, rank, args.secondary_timeout)
 
     if args.only in ("all", "recombine") and args.recombine_batch and L % world == 0:

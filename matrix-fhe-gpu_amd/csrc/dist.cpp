@@ -84,6 +84,9 @@ struct mfhe_comm {
     hipStream_t xs = nullptr;
     hipEvent_t ev_in = nullptr, ev_x[2] = {nullptr, nullptr}, ev_c[2] = {nullptr, nullptr};
     bool c_recorded[2] = {false, false};
+    // a chunked call's exchanges were issued on xs and no reserve has synchronised them since: only then may the next
+    // call skip its ev_in wait (MFHE_RECOMBINE_AFTER_PREV), because xs then runs its exchanges after those
+    bool prev_on_xs = false;
 };
 
 using mfhe::set_error;
@@ -288,9 +291,12 @@ extern "C" int mfhe_crt_recombine_sharded(mfhe_ctx* ctx, mfhe_comm* c, int mode,
     if (int rc = xchg_shape(ctx, c, mode, npoly, ncoeff, &words)) return rc;
     if (npoly == 0 || ncoeff == 0) return MFHE_OK;
     if (!d_shard || !d_out || out_stride == 0) return set_error(MFHE_EINVAL, "recombine: bad pointer / stride");
+    const int G = c->nranks;
+    // world 1: the shard already holds every limb of every polynomial, nothing to exchange
+    if (G == 1) return mfhe_crt_compose_f64_sharded(ctx, d_shard, 1, npoly * (size_t)ctx->L * ncoeff, npoly, ncoeff,
+                                                    d_out, out_stride, s);
     if (int rc = need_rccl()) return rc;
     if (int rc = grow(c, words * sizeof(uint64_t))) return rc;
-    const int G = c->nranks;
     const size_t bs = npoly / G, lg = (size_t)(ctx->L / G);
     const size_t shard = npoly * lg * ncoeff;
     uint64_t* recv = static_cast<uint64_t*>(c->recv);
@@ -331,6 +337,7 @@ extern "C" int mfhe_crt_recombine_chunked_reserve(mfhe_ctx* ctx, mfhe_comm* c, i
             MFHE_HIP(hipEventSynchronize(c->ev_c[b]));
             c->c_recorded[b] = false;
         }
+    c->prev_on_xs = false;
     return grow(c, 2 * words * sizeof(uint64_t));
 }
 
@@ -356,12 +363,24 @@ extern "C" int mfhe_crt_recombine_chunked(mfhe_ctx* ctx, mfhe_comm* c, int mode,
     if (int rc = xchg_shape(ctx, c, mode, npoly, ncoeff, &words)) return rc;   // G | L, G | npoly, mode
     if (npoly == 0 || ncoeff == 0) return MFHE_OK;
     constexpr int kKnown = MFHE_RECOMBINE_ROWS_GLOBAL | MFHE_RECOMBINE_EXCHANGE_ONLY | MFHE_RECOMBINE_AFTER_PREV |
-                           MFHE_RECOMBINE_AGREE | MFHE_RECOMBINE_DEBUG_FAIL;
+                           MFHE_RECOMBINE_AGREE | MFHE_RECOMBINE_COMPOSE_ONLY | MFHE_RECOMBINE_SELF_EXCHANGE |
+                           MFHE_RECOMBINE_DEBUG_FAIL;
     if (!d_shard || (!d_out && !(flags & MFHE_RECOMBINE_EXCHANGE_ONLY)) || out_stride == 0)
         return set_error(MFHE_EINVAL, "recombine: bad pointer / stride");
     if (flags & ~kKnown) return set_error(MFHE_EINVAL, "recombine: unknown flags");
-    if (int rc = need_rccl()) return rc;
+    if ((flags & MFHE_RECOMBINE_EXCHANGE_ONLY) && (flags & MFHE_RECOMBINE_COMPOSE_ONLY))
+        return set_error(MFHE_EINVAL, "recombine: EXCHANGE_ONLY and COMPOSE_ONLY exclude each other");
     const int G = c->nranks;
+    if (G == 1 && !(flags & MFHE_RECOMBINE_SELF_EXCHANGE)) {
+        // world 1: no exchange (the shard holds every limb of every polynomial) -- compose straight from it, all rows at
+        // once (ROWS_GLOBAL and compact rows coincide); the flags keep their meaning
+        if (flags & MFHE_RECOMBINE_DEBUG_FAIL)
+            return set_error(MFHE_EHIP, "recombine: injected compose failure (MFHE_RECOMBINE_DEBUG_FAIL)");
+        if (flags & MFHE_RECOMBINE_EXCHANGE_ONLY) return MFHE_OK;
+        return mfhe_crt_compose_f64_sharded(ctx, d_shard, 1, npoly * (size_t)ctx->L * ncoeff, npoly, ncoeff, d_out,
+                                            out_stride, s);
+    }
+    if (int rc = need_rccl()) return rc;
     const size_t lg = (size_t)(ctx->L / G), cp = chunk_polys_of(chunk_polys, npoly, G);
     size_t cw = 0;
     if (int rc = xchg_shape(ctx, c, mode, cp, ncoeff, &cw)) return rc;
@@ -379,7 +398,12 @@ extern "C" int mfhe_crt_recombine_chunked(mfhe_ctx* ctx, mfhe_comm* c, int mode,
     auto hip = [&](hipError_t he, const char* what) {
         if (he != hipSuccess) fail(mfhe::hip_error(he, what));
     };
-    if (!(flags & MFHE_RECOMBINE_AFTER_PREV)) {
+    const bool xch = !(flags & MFHE_RECOMBINE_COMPOSE_ONLY);
+    if (!xch)   // the composes read what earlier calls' exchanges left in the halves: s is ordered after those
+        for (int b = 0; b < 2; ++b) hip(hipStreamWaitEvent(st, c->ev_x[b], 0), "hipStreamWaitEvent");
+    // AFTER_PREV is only safe behind a previous call's exchanges still ordered on xs; otherwise (the first call, or
+    // the first after a reserve) it is ignored and the exchanges wait for s as usual
+    if (xch && (!(flags & MFHE_RECOMBINE_AFTER_PREV) || !c->prev_on_xs)) {
         hip(hipEventRecord(c->ev_in, st), "hipEventRecord");
         hip(hipStreamWaitEvent(c->xs, c->ev_in, 0), "hipStreamWaitEvent");
     }
@@ -388,23 +412,18 @@ extern "C" int mfhe_crt_recombine_chunked(mfhe_ctx* ctx, mfhe_comm* c, int mode,
         const size_t n = npoly - p0 < cp ? npoly - p0 : cp;   // polys of this chunk (a multiple of G)
         const size_t bs = n / (size_t)G, shard = n * lg * ncoeff;
         const int b = (int)(k & 1);
-        if (c->c_recorded[b]) hip(hipStreamWaitEvent(c->xs, c->ev_c[b], 0), "hipStreamWaitEvent");
         const uint64_t* send = d_shard + p0 * lg * ncoeff;
-        ncclResult_t e;
-        size_t off, stride;
-        if (mode == MFHE_XCHG_ALLGATHER) {
-            e = rccl().AllGather(send, half[b], shard, ncclUint64, c->comm, c->xs);
-            off = (size_t)c->rank * bs * lg * ncoeff;
-            stride = shard;
-        } else {
-            e = rccl().AllToAll(send, half[b], bs * lg * ncoeff, ncclUint64, c->comm, c->xs);
-            off = 0;
-            stride = bs * lg * ncoeff;
+        const bool ag = mode == MFHE_XCHG_ALLGATHER;
+        const size_t off = ag ? (size_t)c->rank * bs * lg * ncoeff : 0, stride = ag ? shard : bs * lg * ncoeff;
+        if (xch) {
+            if (c->c_recorded[b]) hip(hipStreamWaitEvent(c->xs, c->ev_c[b], 0), "hipStreamWaitEvent");
+            const ncclResult_t e = ag ? rccl().AllGather(send, half[b], shard, ncclUint64, c->comm, c->xs)
+                                      : rccl().AllToAll(send, half[b], bs * lg * ncoeff, ncclUint64, c->comm, c->xs);
+            // an RCCL error leaves the communicator unusable (RCCL's own contract): nothing to keep in step with
+            if (e != ncclSuccess) return nccl_error(e, ag ? "ncclAllGather" : "ncclAllToAll");
+            hip(hipEventRecord(c->ev_x[b], c->xs), "hipEventRecord");
+            hip(hipStreamWaitEvent(st, c->ev_x[b], 0), "hipStreamWaitEvent");
         }
-        // an RCCL error leaves the communicator unusable (RCCL's own contract): nothing to keep in step with
-        if (e != ncclSuccess) return nccl_error(e, mode == MFHE_XCHG_ALLGATHER ? "ncclAllGather" : "ncclAllToAll");
-        hip(hipEventRecord(c->ev_x[b], c->xs), "hipEventRecord");
-        hip(hipStreamWaitEvent(st, c->ev_x[b], 0), "hipStreamWaitEvent");
         if ((flags & MFHE_RECOMBINE_DEBUG_FAIL) && k == (npoly > cp ? 1u : 0u))
             fail(set_error(MFHE_EHIP, "recombine: injected compose failure (MFHE_RECOMBINE_DEBUG_FAIL)"));
         if (!err && !(flags & MFHE_RECOMBINE_EXCHANGE_ONLY)) {
@@ -416,6 +435,7 @@ extern "C" int mfhe_crt_recombine_chunked(mfhe_ctx* ctx, mfhe_comm* c, int mode,
         hip(hipEventRecord(c->ev_c[b], st), "hipEventRecord");
         c->c_recorded[b] = true;
     }
+    if (xch) c->prev_on_xs = true;
     if (flags & MFHE_RECOMBINE_AGREE) return mfhe::comm_agree(c, err ? set_error(err, err_msg) : MFHE_OK, st);
     return err ? set_error(err, err_msg) : MFHE_OK;
 }

@@ -923,10 +923,15 @@ static int decode_sharded_impl(mfhe_ctx* c, mfhe_ctx* call, mfhe_comm* comm, int
     const size_t cp = mfhe_ctx::PHI / 4 >= (size_t)G ? mfhe_ctx::PHI / 4 / G * G : (size_t)G;
     RC(wcrt_gemm(c, c->d_wVinv, ev_re, true, coeff_re, WOut::Matrix, false, s, 0, nullptr, 1, dec));
     RC(wcrt_gemm(c, c->d_wVinv, ev_im, true, coeff_im, WOut::Matrix, false, s, 0, nullptr, 1, dec));
-    RC(mfhe_crt_recombine_chunked(call, comm, mode, coeff_re, 512, g.n2, cp, (double*)ccx, 2,
-                                  MFHE_RECOMBINE_ROWS_GLOBAL, (mfhe_stream_t)s));
-    RC(mfhe_crt_recombine_chunked(call, comm, mode, coeff_im, 512, g.n2, cp, (double*)ccx + 1, 2,
-                                  MFHE_RECOMBINE_ROWS_GLOBAL | MFHE_RECOMBINE_AFTER_PREV, (mfhe_stream_t)s));
+    // Both recombines are always issued and their statuses agreed on once at the end: a rank whose re call fails
+    // locally after its exchanges started still joins the im call's collectives and the agreement, so no peer is left
+    // waiting in a collective this rank skipped; every rank then returns the error.
+    const int rre = mfhe_crt_recombine_chunked(call, comm, mode, coeff_re, 512, g.n2, cp, (double*)ccx, 2,
+                                               MFHE_RECOMBINE_ROWS_GLOBAL, (mfhe_stream_t)s);
+    const std::string ere = rre ? mfhe_last_error() : "";
+    const int rim = mfhe_crt_recombine_chunked(call, comm, mode, coeff_im, 512, g.n2, cp, (double*)ccx + 1, 2,
+                                               MFHE_RECOMBINE_ROWS_GLOBAL | MFHE_RECOMBINE_AFTER_PREV, (mfhe_stream_t)s);
+    RC(comm_agree(comm, rre ? set_error(rre, ere) : rim, s));
     for (size_t p0 = 0; p0 < 512; p0 += cp) {
         const size_t bs = (512 - p0 < cp ? 512 - p0 : cp) / (size_t)G;
         RC(comm_allgather_bytes(comm, ccx + (p0 + (size_t)rank * bs) * g.n2, ccx + p0 * g.n2,

@@ -31,6 +31,8 @@ RECOMBINE_ROWS_GLOBAL = 1
 RECOMBINE_EXCHANGE_ONLY = 2     # measurement: exchanges only, composes skipped (out untouched)
 RECOMBINE_AFTER_PREV = 4        # the shard was complete when the previous chunked call on the comm was entered
 RECOMBINE_AGREE = 8             # end with an all-rank status agreement (host wait)
+RECOMBINE_COMPOSE_ONLY = 16     # measurement: composes only, out of the receive halves' last exchanged chunks
+RECOMBINE_SELF_EXCHANGE = 32    # test hook: world 1 runs the exchange pipeline (RCCL self-exchange) anyway
 RECOMBINE_DEBUG_FAIL = 256      # test hook: the compose of chunk 1 (or 0) fails
 OPT_NTT_PACK = 13
 OPT_WCRT_PIPE = 14

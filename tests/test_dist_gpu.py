@@ -1,8 +1,9 @@
 """Native multi-GPU recombine (include/mfhe.h mfhe_comm_* / mfhe_crt_recombine_sharded) on one GPU.
 
-A 1-rank RCCL communicator runs the real exchange code path (ncclAllGather / ncclAllToAll into the
-communicator-owned receive buffer, then the sharded compose) and must equal the unsharded
-mfhe_crt_compose_f64 bit for bit.  RCCL refuses two ranks on one GPU, so the G > 1 layout is pinned by the
+At world 1 the recombine composes straight from the shard (no exchange, r06). The chunked tests pass
+MFHE_RECOMBINE_SELF_EXCHANGE, so a 1-rank RCCL communicator still runs the real exchange code path: ncclAllGather /
+ncclAllToAll into the communicator-owned receive halves, the exchange stream and its events, then the sharded
+compose. Every result must equal the unsharded mfhe_crt_compose_f64 bit for bit.  RCCL refuses two ranks on one GPU, so the G > 1 layout is pinned by the
 gloo tests in test_dist_cpu.py (same offsets and strides) and by the sharded-compose kernel test below,
 which feeds it G shards laid out exactly as the G-rank exchanges deliver them.
 """
@@ -10,6 +11,8 @@ import numpy as np
 import pytest
 
 pytestmark = pytest.mark.gpu
+
+SX = 32   # mfhe.RECOMBINE_SELF_EXCHANGE: world 1 runs the exchange pipeline anyway (tests of the multi-rank machinery)
 
 
 def _residues(rng, npoly, moduli, ncoeff, delta):
@@ -114,12 +117,13 @@ def test_chunked_recombine_one_rank_equals_unsharded(mfhe, orc, mode, rows_globa
         ctx.crt_recombine_chunked_reserve(comm, mode, 4, ncoeff)
         for chunk in (4, 4, 64, 1):
             out = torch.full((npoly * ncoeff,), float("nan"), dtype=torch.float64, device="cuda")
-            ctx.crt_recombine_chunked(comm, mode, d, npoly, ncoeff, chunk, out, rows_global=rows_global)
+            ctx.crt_recombine_chunked(comm, mode, d, npoly, ncoeff, chunk, out, rows_global=rows_global, flags=SX)
             torch.cuda.synchronize()
             assert torch.equal(out, ref), chunk
         # strided output (the decode writes re / im interleaved)
         out2 = torch.full((2 * npoly * ncoeff,), float("nan"), dtype=torch.float64, device="cuda")
-        ctx.crt_recombine_chunked(comm, mode, d, npoly, ncoeff, 3, out2[1:], out_stride=2, rows_global=rows_global)
+        ctx.crt_recombine_chunked(comm, mode, d, npoly, ncoeff, 3, out2[1:], out_stride=2, rows_global=rows_global,
+                                  flags=SX)
         torch.cuda.synchronize()
         assert torch.equal(out2[1::2], ref) and torch.isnan(out2[0::2]).all()
         np.testing.assert_array_equal(ref.cpu().numpy(), v.ravel().astype(np.float64) / ctx.info().delta)
@@ -140,7 +144,7 @@ def test_chunked_recombine_rejects_bad_arguments(mfhe, orc):
             ctx.crt_recombine_chunked(comm, 7, d, 4, 16, 2, out)
         with pytest.raises(mfhe.MfheError):   # unknown flag bits
             mfhe.check(mfhe.lib.mfhe_crt_recombine_chunked(ctx.handle, comm._h, 0, d.data_ptr(), 4, 16, 2,
-                                                           out.data_ptr(), 1, 16, None))
+                                                           out.data_ptr(), 1, 64, None))
         with pytest.raises(ValueError):   # undersized output caught on the host
             ctx.crt_recombine_chunked(comm, "alltoall", d, 4, 16, 2, out[:10])
     finally:
@@ -167,7 +171,7 @@ def test_chunked_recombine_injected_failure_keeps_communicator_usable(mfhe, orc,
     try:
         ctx.crt_recombine_chunked_reserve(comm, "alltoall", 4, ncoeff)
         out = torch.full((npoly * ncoeff,), float("nan"), dtype=torch.float64, device="cuda")
-        flags = mfhe.RECOMBINE_DEBUG_FAIL | (mfhe.RECOMBINE_AGREE if agree else 0)
+        flags = mfhe.RECOMBINE_DEBUG_FAIL | (mfhe.RECOMBINE_AGREE if agree else 0) | SX
         with pytest.raises(mfhe.MfheError, match="injected"):
             ctx.crt_recombine_chunked(comm, "alltoall", d, npoly, ncoeff, 4, out, flags=flags)
         torch.cuda.synchronize()
@@ -176,7 +180,7 @@ def test_chunked_recombine_injected_failure_keeps_communicator_usable(mfhe, orc,
         assert torch.isnan(o[4:]).all()                          # chunks 1, 2: exchanged, not composed
         for _ in range(2):   # the communicator and its receive halves are usable afterwards
             out.fill_(float("nan"))
-            ctx.crt_recombine_chunked(comm, "alltoall", d, npoly, ncoeff, 4, out)
+            ctx.crt_recombine_chunked(comm, "alltoall", d, npoly, ncoeff, 4, out, flags=SX)
             torch.cuda.synchronize()
             assert torch.equal(out, ref)
     finally:
@@ -204,15 +208,92 @@ def test_chunked_recombine_exchange_only_and_after_prev(mfhe, orc):
     try:
         ctx.crt_recombine_chunked_reserve(comm, "allgather", 2, ncoeff)
         out = torch.full((npoly * ncoeff,), float("nan"), dtype=torch.float64, device="cuda")
-        ctx.crt_recombine_chunked(comm, "allgather", d, npoly, ncoeff, 2, out, flags=mfhe.RECOMBINE_EXCHANGE_ONLY)
-        ctx.crt_recombine_chunked(comm, "allgather", d, npoly, ncoeff, 2, None, flags=mfhe.RECOMBINE_EXCHANGE_ONLY)
+        ctx.crt_recombine_chunked(comm, "allgather", d, npoly, ncoeff, 2, out, flags=mfhe.RECOMBINE_EXCHANGE_ONLY | SX)
+        ctx.crt_recombine_chunked(comm, "allgather", d, npoly, ncoeff, 2, None, flags=mfhe.RECOMBINE_EXCHANGE_ONLY | SX)
         torch.cuda.synchronize()
         assert torch.isnan(out).all()
         out2 = torch.full_like(out, float("nan"))
-        ctx.crt_recombine_chunked(comm, "allgather", d, npoly, ncoeff, 2, out)
-        ctx.crt_recombine_chunked(comm, "allgather", d2, npoly, ncoeff, 2, out2, flags=mfhe.RECOMBINE_AFTER_PREV)
+        ctx.crt_recombine_chunked(comm, "allgather", d, npoly, ncoeff, 2, out, flags=SX)
+        ctx.crt_recombine_chunked(comm, "allgather", d2, npoly, ncoeff, 2, out2, flags=mfhe.RECOMBINE_AFTER_PREV | SX)
         torch.cuda.synchronize()
         assert torch.equal(out, ref) and torch.equal(out2, ref2)
+    finally:
+        comm.close()
+        ctx.close()
+
+
+@pytest.mark.parametrize("mode", ["allgather", "alltoall"])
+def test_world1_recombine_composes_from_the_shard(mfhe, orc, mode):
+    """at world 1 the chunked recombine exchanges nothing and composes straight from the shard -- bit
+    for bit the unsharded compose, for every chunk size and both row orders. EXCHANGE_ONLY then does nothing, and
+    DEBUG_FAIL still fails. COMPOSE_ONLY composes. No receive buffer is needed (no reserve is called here)."""
+    import torch
+    moduli = orc.gen_primes(50, 1 << 18, 8)
+    ctx = mfhe.Context(moduli, 16)
+    npoly, ncoeff = 11, 1 << 12
+    res, v = _residues(np.random.default_rng(21), npoly, moduli, ncoeff, ctx.info().delta)
+    d = mfhe.to_device_u64(res.ravel())
+    ref = torch.empty(npoly * ncoeff, dtype=torch.float64, device="cuda")
+    ctx.crt_compose_f64(d, ref, npoly, ncoeff)
+    comm = mfhe.Comm.from_id(mfhe.Comm.unique_id(), 1, 0)
+    try:
+        for chunk in (1, 4, 64):
+            for rows_global in (False, True):
+                for fl in (0, mfhe.RECOMBINE_COMPOSE_ONLY, mfhe.RECOMBINE_AFTER_PREV | mfhe.RECOMBINE_AGREE):
+                    out = torch.full((npoly * ncoeff,), float("nan"), dtype=torch.float64, device="cuda")
+                    ctx.crt_recombine_chunked(comm, mode, d, npoly, ncoeff, chunk, out, rows_global=rows_global,
+                                              flags=fl)
+                    torch.cuda.synchronize()
+                    assert torch.equal(out, ref), (chunk, rows_global, fl)
+        out = torch.full((npoly * ncoeff,), float("nan"), dtype=torch.float64, device="cuda")
+        ctx.crt_recombine_chunked(comm, mode, d, npoly, ncoeff, 4, out, flags=mfhe.RECOMBINE_EXCHANGE_ONLY)
+        ctx.crt_recombine_chunked(comm, mode, d, npoly, ncoeff, 4, None, flags=mfhe.RECOMBINE_EXCHANGE_ONLY)
+        torch.cuda.synchronize()
+        assert torch.isnan(out).all()
+        with pytest.raises(mfhe.MfheError, match="injected"):
+            ctx.crt_recombine_chunked(comm, mode, d, npoly, ncoeff, 4, out, flags=mfhe.RECOMBINE_DEBUG_FAIL)
+        with pytest.raises(mfhe.MfheError):   # the two measurement flags exclude each other
+            ctx.crt_recombine_chunked(comm, mode, d, npoly, ncoeff, 4, out,
+                                      flags=mfhe.RECOMBINE_EXCHANGE_ONLY | mfhe.RECOMBINE_COMPOSE_ONLY)
+        out.zero_()
+        ctx.crt_recombine_sharded(comm, mode, d, npoly - 0, ncoeff, out)   # the one-shot form: also no exchange
+        torch.cuda.synchronize()
+        assert torch.equal(out, ref)
+        np.testing.assert_array_equal(ref.cpu().numpy(), v.ravel().astype(np.float64) / ctx.info().delta)
+    finally:
+        comm.close()
+        ctx.close()
+
+
+def test_compose_only_recomposes_the_halves(mfhe, orc):
+    """MFHE_RECOMBINE_COMPOSE_ONLY (bench.py compose_only_ms) through the exchange pipeline (self-exchange): with two
+    chunks, the halves hold exactly chunks 0 and 1 after a normal call, so a compose-only call reproduces its output
+    bit for bit without exchanging. A later AFTER_PREV call must not rely on a compose-only call's (absent)
+    exchanges: it still equals the plain result."""
+    import torch
+    moduli = orc.gen_primes(50, 1 << 18, 8)
+    ctx = mfhe.Context(moduli, 16)
+    npoly, ncoeff = 8, 1 << 12
+    res, _ = _residues(np.random.default_rng(23), npoly, moduli, ncoeff, ctx.info().delta)
+    d = mfhe.to_device_u64(res.ravel())
+    ref = torch.empty(npoly * ncoeff, dtype=torch.float64, device="cuda")
+    ctx.crt_compose_f64(d, ref, npoly, ncoeff)
+    comm = mfhe.Comm.from_id(mfhe.Comm.unique_id(), 1, 0)
+    try:
+        for mode in ("allgather", "alltoall"):
+            ctx.crt_recombine_chunked_reserve(comm, mode, 4, ncoeff)
+            out = torch.full((npoly * ncoeff,), float("nan"), dtype=torch.float64, device="cuda")
+            ctx.crt_recombine_chunked(comm, mode, d, npoly, ncoeff, 4, out, flags=SX)
+            out2 = torch.full_like(out, float("nan"))
+            ctx.crt_recombine_chunked(comm, mode, d, npoly, ncoeff, 4, out2, flags=SX | mfhe.RECOMBINE_COMPOSE_ONLY)
+            torch.cuda.synchronize()
+            assert torch.equal(out, ref) and torch.equal(out2, ref), mode
+            # after a reserve no exchange is tracked: AFTER_PREV is ignored (the exchanges wait for the stream)
+            ctx.crt_recombine_chunked_reserve(comm, mode, 4, ncoeff)
+            out3 = torch.full_like(out, float("nan"))
+            ctx.crt_recombine_chunked(comm, mode, d, npoly, ncoeff, 4, out3, flags=SX | mfhe.RECOMBINE_AFTER_PREV)
+            torch.cuda.synchronize()
+            assert torch.equal(out3, ref), mode
     finally:
         comm.close()
         ctx.close()
