@@ -48,7 +48,7 @@ def parse():
                     help="skip the reference-geometry pipeline and other-config NTT lines (N=1 only)")
     ap.add_argument("--cpu-seconds", type=float, default=10.0)
     ap.add_argument("--no-c5", action="store_true", help="skip the BASELINE C5 residue-shard line")
-    ap.add_argument("--only", default="all", help="all | ntt | crt | recombine | c4 | c5 (profiling)")
+    ap.add_argument("--only", default="all", help="all | ntt | crt | recombine | c4 | c5 | u64 (profiling)")
     ap.add_argument("--recombine-batch", type=int, default=256,
                     help="polys per step for the residue-shard INTT + CRT recombine line (0 = skip)")
     ap.add_argument("--secondary-timeout", type=float, default=300.0,
@@ -650,8 +650,9 @@ def cpu_baseline(log_n, moduli, seconds):
 
 
 def u64_line(reps=20, warm=3):
-    """C3 forward NTT on the 64-bit integer path (ArithU64, Harvey/Shoup): 60-bit primes, which the FP64 path
-    cannot take (q < 2^50), and the headline's 50-bit primes forced onto U64 for comparison."""
+    """C3 forward and inverse NTT on the 64-bit integer path: 60-bit primes, which the FP64 path cannot take
+    (q < 2^50), and the headline's 50-bit primes forced onto U64 for comparison.  Every q < 2^60 here, so both
+    directions run the lazy U60 schedules (ArithU60); the Harvey schedule (ArithU64, OPT_NTT_U60 0) beside them."""
     import torch
     import mfhe
     log_n, L, batch = 16, 8, 1024
@@ -667,7 +668,8 @@ def u64_line(reps=20, warm=3):
         d.random_(0, 2 ** 62).remainder_(qt)
         del qt
         out = {}
-        for kind, fn in (("fwd", ctx.ntt_fwd), ("inv", ctx.ntt_inv)):
+
+        def rate(fn):
             for _ in range(warm):
                 fn(d, batch=batch)
             torch.cuda.synchronize()
@@ -677,13 +679,20 @@ def u64_line(reps=20, warm=3):
                 fn(d, batch=batch)
             e1.record()
             torch.cuda.synchronize()
-            r = batch * L / (e0.elapsed_time(e1) / reps * 1e-3)
+            return batch * L / (e0.elapsed_time(e1) / reps * 1e-3)
+        for kind, fn in (("fwd", ctx.ntt_fwd), ("inv", ctx.ntt_inv)):
+            r = rate(fn)
             out[f"{kind}_NTT_per_s"] = round(r)
             out[f"{kind}_alg_GBps"] = round(16.0 * N * r / 1e9, 1)
         out["frac_fwd"] = round(out["fwd_alg_GBps"] / HBM_PEAK_GBS, 4)
         out["arith"] = "u64" if ctx.info().arith == mfhe.ARITH_U64 else "f64"
-        if out["arith"] == "u64":   # forward schedule: lazy U60 (every q < 2^60) or Harvey
-            out["fwd_schedule"] = "u60" if ctx.get_option(mfhe.OPT_NTT_U60) else "harvey"
+        if out["arith"] == "u64":   # schedule of both directions: lazy U60 (every q < 2^60) or Harvey
+            out["schedule"] = "u60" if ctx.get_option(mfhe.OPT_NTT_U60) else "harvey"
+            if out["schedule"] == "u60":   # the same box's Harvey schedule, for the A/B (MFHE_OPT_NTT_U60 0)
+                ctx.set_option(mfhe.OPT_NTT_U60, 0)
+                out["harvey_fwd_NTT_per_s"] = round(rate(ctx.ntt_fwd))
+                out["harvey_inv_NTT_per_s"] = round(rate(ctx.ntt_inv))
+                ctx.set_option(mfhe.OPT_NTT_U60, 1)
         out["max_modulus_bits"] = max(moduli).bit_length()
         res[name] = out
         del d
@@ -1013,6 +1022,8 @@ def main():
             out["reference_geometry_pipeline"] = pipeline_line()
             out["other_ntt_configs"] = other_configs_line()
             out["trace_gemm_reference_geometry"] = trace_line()
+            out["u64_path_c3_forward_ntt"] = u64_line()
+        if world == 1 and args.only == "u64":
             out["u64_path_c3_forward_ntt"] = u64_line()
         if world == 1 and not args.no_cpu_baseline and args.only == "all":
             try:

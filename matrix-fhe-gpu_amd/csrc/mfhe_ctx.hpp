@@ -84,7 +84,7 @@ struct mfhe_ctx {
     uint64_t N = 0;
     int conv = 0;
     int arith = MFHE_ARITH_AUTO;  // effective: F64 or U64
-    bool u60_ok = false;          // every modulus < 2^60: U64 forward NTTs may run ArithU60
+    bool u60_ok = false;          // every modulus < 2^60: U64 NTTs may run ArithU60
     int ntt_u60 = 1;              // MFHE_OPT_NTT_U60
     bool f64_ok = false;          // every q < 2^50
     double delta = 0.0;

@@ -14,8 +14,8 @@
 //    Used when any modulus is >= 2^50 and for the phantom fnwt_1d/inwt_1d surface,
 //    whose callers hand us u64 Shoup tables.
 //
-//  * ArithU60 -- the same Shoup products with a lazier reduction schedule, for forward
-//    transforms of contexts whose moduli are all < 2^60 (below).
+//  * ArithU60 -- the same Shoup products with lazier reduction schedules, for forward and
+//    inverse transforms of contexts whose moduli are all < 2^60 (below).
 //
 // All produce canonical [0,q) outputs, so results are bit-identical to each
 // other and to the phantom/reference transforms they restate.
@@ -183,8 +183,8 @@ struct ArithU64 {
     __device__ __forceinline__ uint64_t raw_out(uint64_t x) const { return reduce(x); }
 };
 
-// ArithU60 -- forward transforms when every modulus of the context is < 2^60 (phantom's and SEAL's range):
-// 16q < 2^64 leaves room for a lazier schedule than Harvey's reduce-per-butterfly.
+// ArithU60 -- transforms when every modulus of the context is < 2^60 (phantom's and SEAL's range): 16q < 2^64 leaves
+// room for lazier schedules than Harvey's reduce-per-butterfly.  Forward:
 //  * Values enter a round (an exchange-to-exchange run of <= 4 stages) below 16q.  Only the u inputs of the round's
 //    first stage are reduced, once, to [0, 8q) (one select by 8q); every CT adds at most 2q to the bound of its u
 //    input (u' = u + t, v' = u + 2q - t, t = Shoup product in [0, 2q) for any v < 2^64), so after 4 stages every
@@ -239,7 +239,7 @@ struct ArithU60 : ArithU64 {
     // and the scale, shaded down by 2^-20 relative (> the roundings), keeps k <= floor(x / q) while the total
     // shortfall 16 (2^-20 + 3 * 2^-24) + 2^-27 < 2e-5 keeps k >= floor(x / q) - 1, for every q < 2^60.
     // (r05 took the window as the high word for every q; for q < 2^33 the dropped low word is worth >= 0.5 of a
-    // quotient step and canon returned residues >= q: tests/test_ntt_gpu.py modulus-size sweep)
+    // quotient step and canon returned residues >= q: tests/test_modsize_sweep_gpu.py, tests/test_u60_canon_cpu.py.)
     __device__ __forceinline__ uint64_t canon(uint64_t x) const {
         float f;
         asm("v_cvt_f32_u32 %0, %1" : "=v"(f) : "v"((uint32_t)(x >> sh)));
@@ -253,6 +253,27 @@ struct ArithU60 : ArithU64 {
         r = ((uint64_t)rh << 32) | (uint32_t)r;
         return sel_sub(r, r + nq);
     }
+
+    // ---- the inverse (r06): Gentleman-Sande with X left unreduced ----
+    // An element of bound exponent B is < 2q 2^B.  GS on a pair of equal exponents B (always the case, U60InvBounds):
+    // X = u + v has exponent B + 1; Y = Shoup((u + 2q 2^B) - v, w) is in [0, 2q) (exponent 0) for any input < 2^64,
+    // and (u + 2q 2^B) - v < 2q 2^(B+2) < 2^64 while B <= 2 and q < 2^60.  An exponent-3 pair (16q) is reduced
+    // first.  Harvey (ArithU64::gs) instead reduces X in every butterfly: 32 selects per 4-stage round of 16
+    // registers against 18 here (6 mid-round + 12 at the round's end, U60InvBounds).
+    template <int B>
+    __device__ __forceinline__ uint64_t red(uint64_t x) const {   // exponent B -> 0: B selects by 2q 2^(B-1), .., 2q
+        if constexpr (B > 0) return red<B - 1>(sel_sub(x, x + (n2q << (B - 1))));
+        else return x;
+    }
+    // the inverse's outputs: its last stage leaves every value in [0, 2q) (X = Shoup((u + v), n^-1), Y Shoup too)
+    __device__ __forceinline__ uint64_t canon_inv(uint64_t x) const { return sel_sub(x, x + nq); }
+    template <int B>
+    __device__ __forceinline__ void gs_b(uint64_t& u, uint64_t& v, Tw w) const {
+        static_assert(B >= 0 && B <= 2, "GS input exponent");
+        const uint64_t a = u, b = v;
+        u = a + b;
+        v = mulmod(a + (two_q << B) - b, w);
+    }
 };
 
 template <class A>
@@ -260,6 +281,26 @@ constexpr bool kIsU64 = std::is_base_of<ArithU64, A>::value;   // the 64-bit int
 template <class A>
 constexpr bool kLazyU60 = std::is_same<A, ArithU60>::value;
 
-
+// Bound exponents of the lazy U60 inverse (ArithU60::gs_b) over one round: R registers, executed stages bb = 0, 1, ..
+// (stage bb pairs k, k + 2^bb; X -> k, Y -> k + 2^bb).  All exponents are 0 when a round starts.  The two elements of
+// a pair have the same history (they differ only in bit bb, no earlier stage's bit), hence equal exponents.  An
+// exponent-3 pair is reduced before its butterfly.  R = 16: exponents after 4 stages {1,3,2,2,1,1,1,1, 0 x 8}.
+template <int R>
+struct U60InvBounds {
+    // exponent of element k after the first n executed stages of a round
+    static constexpr int after(int k, int n) {
+        int B[R] = {};
+        for (int bb = 0; bb < n; ++bb) {
+            const int h = 1 << bb;
+            for (int j = 0; j < R; ++j) {
+                if (j & h) continue;
+                const int e = B[j] == 3 ? 0 : B[j];
+                B[j] = e + 1;
+                B[j + h] = 0;
+            }
+        }
+        return B[k];
+    }
+};
 
 }  // namespace mfhe

@@ -158,6 +158,32 @@ __device__ __forceinline__ void coldb_tile_inv(uint64_t* buf, uint32_t gl, uint3
     typename A::T x[C::R];
 #pragma unroll
     for (int k = 0; k < C::R; ++k) x[k] = A::from_raw(buf[(size_t)Gm::g_of(1, tau, k) * C::NG + gl]);
+    if constexpr (kLazyU60<A>) {
+        // the lazy U60 inverse (ntt_arith.hpp ArithU60::gs_b, U60InvBounds): the same two rounds with X unreduced
+        static_for<0, 4>([&](auto bi) {
+            constexpr int bb = decltype(bi)::value, e = 3 - bb;
+            u60_inv_stage<C::R, bb, false>(ar, x, [&](int k) { return tw1[(1 << e) - 1 + (k >> (bb + 1))]; },
+                                           typename A::Tw{});
+        });
+        u60_inv_round_end<C::R, 4>(ar, x);
+        lds_barrier();
+#pragma unroll
+        for (int k = 0; k < C::R; ++k) my[Gm::pad(Gm::g_of(1, tau, k))] = A::to_raw(x[k]);
+        lds_barrier();
+#pragma unroll
+        for (int k = 0; k < C::R; ++k) x[k] = A::from_raw(my[Gm::pad(Gm::g_of(0, tau, k))]);
+        after_reads();
+        static_for<0, 4>([&](auto bi) {
+            constexpr int bb = decltype(bi)::value, e = 3 - bb;
+            if constexpr (bb == 3) {
+                const auto w1 = tw0[0];
+                u60_inv_stage<C::R, bb, true>(ar, x, [&](int) { return w1; }, ninv);
+            } else {
+                u60_inv_stage<C::R, bb, false>(ar, x, [&](int k) { return tw0[(1 << e) - 1 + (k >> (bb + 1))]; },
+                                               typename A::Tw{});
+            }
+        });
+    } else {
     // round 1: stages 7..4 (register bits 0..3); executed stages 0..3 of the pass: even -> lazy GS
     static_for<0, 4>([&](auto bi) {
         constexpr int bb = decltype(bi)::value, e = 3 - bb, half = 1 << bb;
@@ -200,6 +226,7 @@ __device__ __forceinline__ void coldb_tile_inv(uint64_t* buf, uint32_t gl, uint3
             }
         }
     });
+    }
     // base is workgroup-uniform; say so (the U64 kernel otherwise wraps every store in a readfirstlane loop)
     const uint64_t bu = (uint64_t)base;
     uint64_t* const ubase = (uint64_t*)(((uint64_t)(uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)(bu >> 32)) << 32) |
@@ -208,7 +235,7 @@ __device__ __forceinline__ void coldb_tile_inv(uint64_t* buf, uint32_t gl, uint3
 #pragma unroll
     for (int k = 0; k < C::R; ++k)
         __builtin_amdgcn_raw_buffer_store_b64(
-            __builtin_bit_cast(__attribute__((ext_vector_type(2))) unsigned, ar.canon(x[k])), rs,
+            __builtin_bit_cast(__attribute__((ext_vector_type(2))) unsigned, inv_out(ar, x[k])), rs,
             (int)((off0 | ((uint32_t)Gm::g_of(0, tau, k) << logS)) * 8u), 0, MFHE_NTT_CPOL_INV_COL_OUT);
 }
 

@@ -110,6 +110,43 @@ __device__ __forceinline__ void static_for(F&& f) {
     }
 }
 
+// One lazy U60 inverse butterfly stage on registers x[0..R): executed stage bb of its round, twiddle of pair k from
+// tw(k), X scaled by wn instead when LAST (the s = 0 stage: X = (u + v) n^-1 in [0, 2q), Y = (u - v) itw[1]).
+template <int R, int BB, bool LAST, class A, class T, class TWF>
+__device__ __forceinline__ void u60_inv_stage(const A& ar, T (&x)[R], TWF&& tw, typename A::Tw wn) {
+    constexpr int half = 1 << BB;
+    static_for<0, R>([&](auto kc) {
+        constexpr int k = decltype(kc)::value;
+        if constexpr (!(k & half)) {
+            constexpr int e0 = U60InvBounds<R>::after(k, BB);
+            constexpr int e = e0 == 3 ? 0 : e0;
+            if constexpr (e0 == 3) {
+                x[k] = ar.template red<3>(x[k]);
+                x[k + half] = ar.template red<3>(x[k + half]);
+            }
+            const auto w = tw(k);
+            ar.template gs_b<e>(x[k], x[k + half], w);
+            if constexpr (LAST) x[k] = ar.mulmod(x[k], wn);
+        }
+    });
+}
+
+// canonical output of an inverse pass that ran the transform's last stage (s = 0): < 2q under the lazy U60 inverse
+template <class A>
+__device__ __forceinline__ uint64_t inv_out(const A& ar, typename A::T x) {
+    if constexpr (kLazyU60<A>) return ar.canon_inv(x);
+    else return ar.canon(x);
+}
+
+// the end of a lazy U60 inverse round of n executed stages: every element back to exponent 0 (< 2q)
+template <int R, int N, class A, class T>
+__device__ __forceinline__ void u60_inv_round_end(const A& ar, T (&x)[R]) {
+    static_for<0, R>([&](auto kc) {
+        constexpr int k = decltype(kc)::value;
+        x[k] = ar.template red<U60InvBounds<R>::after(k, N)>(x[k]);
+    });
+}
+
 // Where one tile (NG groups) of a pass lives: limb/batch, base pointer, twiddle offset, (hi, lo).
 // UNI: every group of the tile lies in one polynomial (two-pass plans; single pass with NG = 1), so the
 // base pointer is workgroup-uniform and each element address is an SGPR base + 32-bit lane offset.
@@ -396,7 +433,20 @@ struct NttPass {
                     constexpr int ri = NR - 1 - r;
                     constexpr int first = (Gm::HB(NR - 1) < LOG_R - 1 ? Gm::HB(NR - 1) : LOG_R - 1) + 1;
                     constexpr int e = ri == 0 ? bb : first + (ri - 1) * LOG_R + bb;
-                    if (s == 0) {
+                    if constexpr (kLazyU60<A>) {
+                        // lazy U60 inverse: X unreduced, per-register bound exponents (U60InvBounds; bb is the
+                        // executed-stage index of this round: a round's executed stages are bb = 0, 1, ..)
+                        if (s == 0) {
+                            const Tw wn = a.ninv.get((size_t)L.mod);
+                            const Tw w1 = a.tw.get(twoff + 1);
+                            u60_inv_stage<R, bb, true>(ar, x, [&](int) { return w1; }, wn);
+                        } else {
+                            u60_inv_stage<R, bb, false>(ar, x, [&](int k) {
+                                if constexpr (kTwPre && r == NR - 1 && bb == 0) return wpre[k >> 1];
+                                else return a.tw.get(twb + (uint64_t)(k >> (bb + 1)));
+                            }, Tw{});
+                        }
+                    } else if (s == 0) {
                         const Tw wn = a.ninv.get((size_t)L.mod);
                         const Tw w1 = a.tw.get(twoff + 1);
 #pragma unroll
@@ -440,6 +490,13 @@ struct NttPass {
                 if constexpr (r < NR - 1)
                     exchange(std::integral_constant<int, r + 1>{}, std::integral_constant<int, r>{}, false);
                 static_for<0, LOG_R>([&](auto bi) { stage(std::integral_constant<int, r>{}, bi); });
+                if constexpr (kLazyU60<A>) {
+                    // back to < 2q before an exchange or a raw intermediate store (the next round / pass starts
+                    // at exponent 0); a canonical store takes up to 16q (ArithU60::canon) as it is
+                    constexpr int hb = Gm::HB(r), wl = Gm::WL(r);
+                    constexpr int nexec = (hb - wl + 1) < LOG_R ? (hb - wl + 1) : LOG_R;
+                    if constexpr (r > 0 || OUT_RAW) u60_inv_round_end<R, nexec>(ar, x);
+                }
             });
         }
 
@@ -486,7 +543,7 @@ struct NttPass {
                     const uint32_t g = Gm::g_of(r_store, tau_, k);
                     T y = x[k];
                     if constexpr (TWIST && INV) y = ar.mulmod(y, a.twist.get(twoff + jidx(L, g)));
-                    const uint64_t o = OUT_RAW ? ar.raw_out(y) : ar.canon(y);
+                    const uint64_t o = OUT_RAW ? ar.raw_out(y) : INV ? inv_out(ar, y) : ar.canon(y);
                     __builtin_amdgcn_raw_buffer_store_b64(__builtin_bit_cast(__attribute__((ext_vector_type(2))) unsigned, o),
                                                           rs, (int)(jidx(L, g) * 8u), 0, kCpolSt);
                 }
@@ -499,7 +556,7 @@ struct NttPass {
 #ifdef MFHE_EXP_SKIP
                     if (OUT_RAW && k >= 12) continue;   // traffic experiment only (wrong results)
 #endif
-                    L.base[jidx(L, g)] = OUT_RAW ? ar.raw_out(y) : ar.canon(y);
+                    L.base[jidx(L, g)] = OUT_RAW ? ar.raw_out(y) : INV ? inv_out(ar, y) : ar.canon(y);
                 }
             }
         }

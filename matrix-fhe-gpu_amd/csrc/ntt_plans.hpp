@@ -361,5 +361,6 @@ extern template int run_kind<ArithF64, TwSrcF, true>(const NttJob<TwSrcF>&, Kind
 extern template int run_kind<ArithU64, TwSrcU, false>(const NttJob<TwSrcU>&, Kind, hipStream_t);
 extern template int run_kind<ArithU64, TwSrcU, true>(const NttJob<TwSrcU>&, Kind, hipStream_t);
 extern template int run_kind<ArithU60, TwSrcU, false>(const NttJob<TwSrcU>&, Kind, hipStream_t);
+extern template int run_kind<ArithU60, TwSrcU, true>(const NttJob<TwSrcU>&, Kind, hipStream_t);
 
 }  // namespace mfhe

@@ -57,9 +57,10 @@ def _kernel_asm(symbol_re: str) -> str:
     pytest.fail(f"kernel {symbol_re} not found in {LIB}")
 
 
-@pytest.mark.parametrize("arith,inv", [("F64", False), ("F64", True), ("U64", False), ("U64", True), ("U60", False)],
+@pytest.mark.parametrize("arith,inv", [("F64", False), ("F64", True), ("U64", False), ("U64", True), ("U60", False),
+                                       ("U60", True)],
                          ids=["F64-forward-first-pass", "F64-inverse-last-pass", "U64-forward-first-pass",
-                              "U64-inverse-last-pass", "U60-forward-first-pass"])
+                              "U64-inverse-last-pass", "U60-forward-first-pass", "U60-inverse-last-pass"])
 def test_column_pass_dma_waits_match_the_instruction_mix(inv, arith):
     sb = arith != "F64"   # the U64 / U60 column pass runs the single-buffer form (ntt_plans.hpp col_db_single)
     asm = _kernel_asm(r"_ZN4mfhe17ntt_col_db_kernelINS_8Arith" + arith + r"ENS_6TwSrc" + arith[0] +
