@@ -704,9 +704,8 @@ extern "C" int mfhe_ctx_set_option(mfhe_ctx* c, int opt, int64_t v) {
             if (v < 0 || v > 1) return set_error(MFHE_EINVAL, "enc a direct must be 0 or 1");
             c->enc_a_direct = (int)v;
             return MFHE_OK;
-        case MFHE_OPT_DEC_MM:
-            if (v < 0 || v > 1) return set_error(MFHE_EINVAL, "dec mm must be 0 or 1");
-            c->dec_mm = (int)v;
+        case MFHE_OPT_DEC_MM:   // the decrypt's ring product on the matrix cores (r05): measured 2.4x slower, removed in r06
+            if (v != 0) return set_error(MFHE_EINVAL, "MFHE_OPT_DEC_MM was removed in r06: only 0 is accepted");
             return MFHE_OK;
         case MFHE_OPT_HE_STREAMS:
             if (v < 0 || v > 3) return set_error(MFHE_EINVAL, "he streams must be 0, 1, 2 or 3");
@@ -764,7 +763,7 @@ extern "C" int mfhe_ctx_get_option(const mfhe_ctx* c, int opt, int64_t* v) {
         case MFHE_OPT_NTT_U60: *v = c->ntt_u60 && c->u60_ok; return MFHE_OK;
         case MFHE_OPT_HE_STREAMS: *v = c->he_streams; return MFHE_OK;
         case MFHE_OPT_ENC_A_DIRECT: *v = c->enc_a_direct; return MFHE_OK;
-        case MFHE_OPT_DEC_MM: *v = c->dec_mm; return MFHE_OK;
+        case MFHE_OPT_DEC_MM: *v = 0; return MFHE_OK;
         default: return set_error(MFHE_EINVAL, "unknown option");
     }
 }

@@ -1026,266 +1026,6 @@ __global__ __launch_bounds__(256) void dec_colsum_pair_kernel(ModGemmArgs a, Mod
     dec_colsum_impl(hi ? b : a, Ppad, G, hi ? y - L : y, L);
 }
 
-// ---- the decrypt-fused digitize with the ring product on the matrix cores (MFHE_OPT_DEC_MM) ----
-// For one (w, l) the 64 X rows y of ct.a all meet the same s, so the ring product of HE.cu:1575-1590 (X-NTT, * s,
-// X-INTT) over them is one matrix product T_w = A_w M_s with the negacyclic matrix of s in coefficient form:
-//   M_s[k][x] = s[x - k] (k <= x), -s[x - k + 64] (k > x),
-// exact through balanced i8 digits as the W-CRT GEMM above (v_mfma_i32_16x16x64_i8 over the D x D digit pairs, the
-// same FP64 epilogue), instead of ~1,500 FP64 instructions per lane and panel of butterflies.
-// Workgroup: limb l, panel kc, quarter (a', hf) = the 16 k (= w) at byte offset (2 a' + hf) 16 of each column's
-// 64-byte group, rows y in [16 yg, 16 yg + 16), i.e. 1024 columns p = 64 y + x; wave v takes x in [16 v, 16 v + 16).
-// Per w (kk = 15 .. 0, the Horner order): each wave digitizes a quarter of A_w (16 rows x 16 k) into the LDS tile,
-// reads its B fragments out of F (below), 25 / 36 MFMAs, then the epilogue: v = ct.b + T mod q (centred), its digit
-// bytes packed in registers (16 k = 16 bytes per column and plane after the loop) and the column sums as the
-// digitize above (Horner in x1, x2, the plain sum).  The four quarters of one (l, kc, yg) write the four 16-byte
-// parts of the same 64-byte groups: their workgroups are given block ids on one XCD (the L2 that merges them).
-// F[w][digit][m], m = k - x + 63: s[63 - m] (m <= 63), -s[127 - m] (m > 63): lane (x, g) needs the 16 bytes
-// F[16 g - x + 63 ..], read as five dwords and funnel-shifted (v_alignbyte) by its offset mod 4.
-#ifndef MFHE_DMM_KW
-#define MFHE_DMM_KW 16   // w per dec_mm_digitize_kernel workgroup: 16 (a quarter) or 8 (half of one, 2 workgroups / CU)
-#endif
-#ifndef MFHE_DMM_WG_CU
-#define MFHE_DMM_WG_CU (MFHE_DMM_KW == 16 ? 1 : 2)   // launch bound (the LDS stage allows one at 16 w)
-#endif
-#ifndef MFHE_DMM_AHEAD
-#define MFHE_DMM_AHEAD 3   // iterations of lookahead of dec_mm_digitize_kernel's loads (1 or 3)
-#endif
-#ifndef MFHE_DMM_SCHED
-#define MFHE_DMM_SCHED 1
-#endif
-constexpr int DMM_RS = 80;   // A tile row stride in bytes (16 B of padding: rows of one read spread over banks)
-constexpr int DMM_KW = MFHE_DMM_KW;
-static_assert(DMM_KW == 16 || DMM_KW == 8, "16 or 8 w per workgroup");
-template <int D>
-__device__ __forceinline__ void dec_mm_impl(const ModGemmArgs& a, uint32_t Ppad, const PlaneCounts& pc, const int l,
-                                            const int L, const int kc, const int ap, const int hf, const int yg,
-                                            const int half) {
-    constexpr int N = 64, NS = 2 * D - 1, NZ = (NS + 1) / 2, NY = (NZ + 1) / 2, KW = DMM_KW;
-    __shared__ __attribute__((aligned(16))) uint32_t ftab[KW][D][32];
-    __shared__ __attribute__((aligned(16))) uint32_t atab[2][D][16][DMM_RS / 4];
-    // the digit bytes of this quarter: [plane][column of the workgroup][16 k], written out once at the end so each
-    // 64-byte group is completed by the four quarters' workgroups at about the same time (4-byte stores spread over
-    // the kernel's life left partial lines to be evicted: 3-4x slower)
-    __shared__ __attribute__((aligned(16))) uint32_t dstage[D][1024][KW / 4];
-    const int t = threadIdx.x, lane = t & 63, wv = t >> 6;
-    typedef const __attribute__((address_space(4))) double* cdp_t;
-    const cdp_t fo = (cdp_t)(a.ifold + (uint64_t)l * 16);
-    LimbConst lc;
-    lc.qf = fo[0];
-    lc.qinv = fo[1];
-    const ArithF64 ar(lc);
-    const double q = lc.qf;
-    const cdp_t ep = (cdp_t)(a.epi + (uint64_t)l * 8);
-    const double c32[3] = {ep[2], ep[3], ep[4]};
-    const cdp_t izl = (cdp_t)(a.iz + (uint64_t)l * 48);
-    const double x1 = izl[0], x2 = izl[1];
-    const uint64_t w0 = (uint64_t)ap * FK + kc * 32 + hf * 16 + half * 8;   // w of kk = 0
-    const uint64_t* __restrict__ cta = a.dct + a.dtotal;
-    // F tables of the KW w: thread (kk, EPT entries)
-    {
-        constexpr int TPW = 256 / KW, EPT = 128 / TPW;
-        const int kk = t / TPW, m0 = (t % TPW) * EPT;
-        const uint64_t* sc = a.dskc + ((w0 + kk) * L + l) * N;
-        uint32_t dw[D][EPT / 4];
-#pragma unroll
-        for (int i = 0; i < D; ++i)
-#pragma unroll
-            for (int c = 0; c < EPT / 4; ++c) dw[i][c] = 0;
-        uint64_t sv[EPT];
-#pragma unroll
-        for (int e = 0; e < EPT; ++e) {   // every load unconditional (a load under a branch waits at once)
-            const int m = m0 + e;
-            sv[e] = sc[m <= 63 ? 63 - m : (m <= 126 ? 127 - m : 0)];
-        }
-#pragma unroll
-        for (int e = 0; e < EPT; ++e) {
-            const int m = m0 + e;
-            const double c = centred_f(sv[e], q);
-            const double v = m <= 63 ? c : (m <= 126 ? -c : 0.0);
-            const uint64_t bb = balanced_bytes<D>(v);
-#pragma unroll
-            for (int i = 0; i < D; ++i) dw[i][e >> 2] |= ((uint32_t)(bb >> (8 * i)) & 255u) << (8 * (e & 3));
-        }
-#pragma unroll
-        for (int i = 0; i < D; ++i)
-#pragma unroll
-            for (int c = 0; c < EPT / 4; ++c) ftab[kk][i][m0 / 4 + c] = dw[i][c] ^ 0x80808080u;
-    }
-    // this lane's A quarter: row r, k = 16 wv + 4 sub + e
-    const int ar_r = lane & 15, ar_s = lane >> 4;
-    const uint64_t arow = (uint64_t)(16 * yg + ar_r) * N + 16 * wv + 4 * ar_s;
-    auto a_store = [&](int buf, const uint64_t (&av)[4]) {
-        uint32_t pk[D];
-#pragma unroll
-        for (int i = 0; i < D; ++i) pk[i] = 0;
-#pragma unroll
-        for (int e = 0; e < 4; ++e) {
-            const uint64_t bb = balanced_bytes<D>(centred_f(av[e], q));
-#pragma unroll
-            for (int i = 0; i < D; ++i) pk[i] |= ((uint32_t)(bb >> (8 * i)) & 255u) << (8 * e);
-        }
-#pragma unroll
-        for (int i = 0; i < D; ++i) atab[buf][i][ar_r][4 * wv + ar_s] = pk[i] ^ 0x80808080u;
-    };
-    // software pipeline over register rings of MFHE_DMM_AHEAD + 1 slots: A of w(it + 1 + AHEAD) and b of w(it + AHEAD)
-    // are issued at iteration it (one workgroup per CU: the loads in flight have to cover the memory latency); the
-    // per-iteration barrier is a raw s_barrier (LDS ordered by lgkmcnt(0)) so they stay in flight across it
-    constexpr int AH = MFHE_DMM_AHEAD, RS = AH + 1;
-    static_assert(4 % RS == 0, "the ring's slot of an iteration is compile-time within a block of four");
-    auto barrier = []() { asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory"); };
-    auto a_ptr = [&](int kk) { return cta + ((w0 + kk) * L + l) * (uint64_t)(N * N) + arow; };
-    uint64_t an[RS][4], bv[RS][4];
-    {
-        uint64_t av[4];
-        ld4(a_ptr(KW - 1), av);
-#pragma unroll
-        for (int k = 1; k <= AH; ++k) ld4(a_ptr(KW - 1 - k), an[k % RS]);
-        a_store(0, av);
-    }
-    // output lane: column x = 16 wv + (lane & 15), rows y = 16 yg + 4 (lane >> 4) + rr
-    const int ox = 16 * wv + (lane & 15), oy = 16 * yg + 4 * (lane >> 4);
-    const int S = 16 * (lane >> 4) - ox + 63, sdw = S >> 2, ssh = S & 3;
-    // digit bytes of 4 k per (row, plane): one dword into the stage when complete
-    uint32_t pk[4][D];
-    const int nd = l < 64 ? pc.n[l] : D;
-    double h1[4], h2[4], t0[4];
-    auto b_load = [&](int kk, uint64_t (&d)[4]) {
-        const uint64_t* bp = a.dct + ((w0 + kk) * L + l) * (uint64_t)(N * N) + (uint64_t)oy * N + ox;
-#pragma unroll
-        for (int rr = 0; rr < 4; ++rr) d[rr] = bp[rr * N];
-    };
-#pragma unroll
-    for (int k = 0; k < AH; ++k) b_load(KW - 1 - k, bv[k % RS]);
-#pragma unroll
-    for (int rr = 0; rr < 4; ++rr) h1[rr] = h2[rr] = t0[rr] = 0.0;
-    __syncthreads();
-    // blocks of four w: a dword of digit bytes per (row, plane) completes in each block
-#pragma unroll 1
-    for (int blk = 0; blk < KW / 4; ++blk) {
-#pragma unroll
-    for (int i4 = 0; i4 < 4; ++i4) {
-        const int it = 4 * blk + i4, kk = KW - 1 - it, buf = i4 & 1;
-        v4i af[D];
-#pragma unroll
-        for (int i = 0; i < D; ++i) af[i] = *(const v4i*)&atab[buf][i][lane & 15][4 * (lane >> 4)];
-        v4i acc[NS];
-#pragma unroll
-        for (int s = 0; s < NS; ++s) acc[s] = v4i{0, 0, 0, 0};
-        // one B digit plane at a time (its fragment is dead after its D MFMAs)
-#pragma unroll
-        for (int j = 0; j < D; ++j) {
-            const uint32_t* fr = &ftab[kk][j][sdw];
-            const uint32_t d0 = fr[0], d1 = fr[1], d2 = fr[2], d3 = fr[3], d4 = fr[4];
-            const v4i bf = v4i{(int)__builtin_amdgcn_alignbyte(d1, d0, ssh), (int)__builtin_amdgcn_alignbyte(d2, d1, ssh),
-                               (int)__builtin_amdgcn_alignbyte(d3, d2, ssh), (int)__builtin_amdgcn_alignbyte(d4, d3, ssh)};
-#pragma unroll
-            for (int i = 0; i < D; ++i)
-                acc[i + j] = __builtin_amdgcn_mfma_i32_16x16x64_i8(af[i], bf, acc[i + j], 0, 0, 0);
-        }
-#if MFHE_DMM_SCHED
-        __builtin_amdgcn_sched_barrier(0);   // the epilogue's FP64 chains stay after the MFMAs (register pressure)
-#endif
-        if (it < KW - 1) a_store(buf ^ 1, an[(i4 + 1) % RS]);
-#pragma unroll
-        for (int rr = 0; rr < 4; ++rr) {
-            double z[NZ];
-#pragma unroll
-            for (int u = 0; u < NZ; ++u)
-                z[u] = 2 * u + 1 < NS ? __fma_rn(256.0, (double)acc[2 * u + 1][rr], (double)acc[2 * u][rr])
-                                      : (double)acc[2 * u][rr];
-            double tv = ArithF64::from_u64(bv[i4 % RS][rr]);
-#pragma unroll
-            for (int u = 0; u < NY; ++u) {
-                const double y = 2 * u + 1 < NZ ? __fma_rn(65536.0, z[2 * u + 1], z[2 * u]) : z[2 * u];
-                tv += u == 0 ? y : ar.mulmod(y, c32[u - 1]);
-            }
-            const double v = ar.reduce(tv);
-            h1[rr] = ar.mulmod(h1[rr], x1) + v;   // from 0: the first step is exact (mulmod(0, .) = 0)
-            h2[rr] = ar.mulmod(h2[rr], x2) + v;
-            t0[rr] += v;
-            const uint64_t bb = balanced_bytes<D>(v);
-#pragma unroll
-            for (int i = 0; i < D; ++i) {
-                const uint32_t by = ((uint32_t)(bb >> (8 * i)) & 255u) << (8 * (3 - i4));
-                pk[rr][i] = i4 == 0 ? by : pk[rr][i] | by;
-            }
-            if (i4 == 3) {
-                const int cl = (oy - 16 * yg + rr) * N + ox;   // column within the workgroup
-#pragma unroll
-                for (int i = 0; i < D; ++i) dstage[i][cl][kk >> 2] = pk[rr][i] ^ 0x80808080u;
-            }
-        }
-        // the next loads into the slots just consumed: in flight across the next AH barriers
-        if (it + 1 + AH <= KW - 1) ld4(a_ptr(kk - 1 - AH), an[(i4 + 1 + AH) % RS]);
-        if (it + AH <= KW - 1) b_load(kk - AH, bv[(i4 + AH) % RS]);
-        barrier();   // the A tile just written is read next; the one read here is rewritten after
-    }
-    }
-    // the stage out: thread = column, 16-byte stores (a wave covers 64 consecutive columns' chunks)
-    __syncthreads();
-    {
-        int8_t* const bdl = a.Bdig + ((uint64_t)l * D * (FK / 32) + kc) * (uint64_t)Ppad * 64 + (2 * ap + hf) * 16 +
-                            half * 8 + (uint64_t)(16 * yg * N) * 64;
-#pragma unroll
-        for (int i = 0; i < D; ++i) {
-            if (i >= nd) break;
-#pragma unroll
-            for (int c4 = 0; c4 < 4; ++c4) {
-                const int cl = c4 * 256 + t;
-                int8_t* o = bdl + (uint64_t)i * (FK / 32) * Ppad * 64 + (uint64_t)cl * 64;
-                if constexpr (KW == 16) *(v4i*)o = *(const v4i*)dstage[i][cl];
-                else *(uint2*)o = *(const uint2*)dstage[i][cl];
-            }
-        }
-    }
-    const cdp_t zp = izl + 16;
-    const int ch = 2 * kc + hf;   // the chunk of 16 k: its power of x1 / x2 (as k0 >> 4 in the digitize above)
-    double z1 = zp[ch], z2 = zp[16 + ch];
-    if (KW == 8 && half) {   // the upper 8 k of the chunk: x^8 more (three exact squarings)
-        double e1 = x1, e2 = x2;
-#pragma unroll
-        for (int s = 0; s < 3; ++s) {
-            e1 = ar.mulmod(e1, e1);
-            e2 = ar.mulmod(e2, e2);
-        }
-        z1 = ar.mulmod(z1, e1);
-        z2 = ar.mulmod(z2, e2);
-    }
-    const int share = ch * (16 / KW) + half;
-#pragma unroll
-    for (int rr = 0; rr < 4; ++rr) {
-        const uint32_t p = (uint32_t)(oy + rr) * N + ox;
-        double* po = a.dpart + (((uint64_t)share * L + l) * Ppad + p) * 6 + ap * 3;
-        po[0] = ar.reduce(t0[rr]);
-        po[1] = ar.reduce(ar.mulmod(h1[rr], z1));
-        po[2] = ar.reduce(ar.mulmod(h2[rr], z2));
-    }
-}
-// block b -> (limb, panel, row group, sub): the NSUB workgroups (a', hf[, half]) of one (l, kc, yg) get ids 8 apart (one
-// XCD: its L2 merges their parts of each 64-byte group)
-constexpr int DMM_NSUB = 4 * 16 / DMM_KW;
-struct DecMmBlock {
-    int lz, kc, yg, ap, hf, half;
-};
-__device__ __forceinline__ DecMmBlock dec_mm_block() {
-    const uint32_t b = blockIdx.x, j = b >> 3, g = (j / DMM_NSUB) * 8 + (b & 7), sb = j % DMM_NSUB;
-    const uint32_t qd = DMM_KW == 16 ? sb : sb >> 1;
-    return DecMmBlock{(int)(g >> 5), (int)((g >> 2) & 7), (int)(g & 3), (int)(qd >> 1), (int)(qd & 1),
-                      DMM_KW == 16 ? 0 : (int)(sb & 1)};
-}
-template <int D>
-__global__ __launch_bounds__(256, MFHE_DMM_WG_CU) void dec_mm_digitize_kernel(ModGemmArgs a, uint32_t Ppad, PlaneCounts pc, int L) {
-    const DecMmBlock k = dec_mm_block();
-    dec_mm_impl<D>(a, Ppad, pc, k.lz, L, k.kc, k.ap, k.hf, k.yg, k.half);
-}
-template <int D>
-__global__ __launch_bounds__(256, MFHE_DMM_WG_CU) void dec_mm_digitize_pair_kernel(ModGemmArgs a, ModGemmArgs b, uint32_t Ppad,
-                                                                      PlaneCounts pc, int L) {
-    const DecMmBlock k = dec_mm_block();
-    const bool hi = k.lz >= L;
-    dec_mm_impl<D>(hi ? b : a, Ppad, pc, hi ? k.lz - L : k.lz, L, k.kc, k.ap, k.hf, k.yg, k.half);
-}
-constexpr int DMM_G = 16 * 16 / DMM_KW;   // column-sum shares of dec_mm_digitize_kernel: one per (kc, hf[, half])
 
 // C = sum_s acc_s * 256^s mod q for the 32 x 32 wave tile at (m0, p0) of limb l (lane = (r, h)).
 // MODE 1 (factored forward): column p0 + r is (a', p) = divmod(., Ppad), output row a' * 256 + row, plus d0.
@@ -1445,7 +1185,10 @@ __device__ __forceinline__ void mfma_epilogue(const ModGemmArgs& a, const v16i (
     if constexpr (FAC) return;   // factored mode always has the FP64 epilogue (launch_mod_gemm checks)
     typedef const __attribute__((address_space(4))) uint64_t* cup_t;
     const uint64_t q = ((cup_t)a.qmu)[2 * l], mu = ((cup_t)a.qmu)[2 * l + 1];
-    const cup_t rt = (cup_t)(a.rtab + (uint64_t)l * NS * 2);
+    // rtab rows are [L][2 a.D - 1][2] for the context's plane stride a.D: a limb run with fewer digits (NS < 2 a.D - 1)
+    // must still step by the table's row length (r06: stepping by NS gave limbs >= 1 of a D = 7 run in a D = 8 context
+    // another limb's constants, tests/test_wcrt_sizes_gpu.py at 55 bits)
+    const cup_t rt = (cup_t)(a.rtab + (uint64_t)l * (2 * a.D - 1) * 2);
     uint64_t* C = Cl;
     const uint32_t col = p0 + r;
     if (col >= a.P) return;
@@ -1759,7 +1502,7 @@ static void launch_staged(int pipe, dim3 grid, hipStream_t s, const ModGemmArgs&
 size_t mod_gemm_mfma_ws(uint32_t P, int L, int D) {
     const uint64_t Ppad = ((uint64_t)P + 63) / 64 * 64;
     // digit planes, then the factored d0 / (c0, c1), then the split decrypt-fused digitize's column partials
-    return (size_t)L * D * Ppad * MK + (size_t)L * 2 * Ppad * 8 + (size_t)std::max(MFHE_DEC_SPLIT, DMM_G) * L * Ppad * 6 * 8;
+    return (size_t)L * D * Ppad * MK + (size_t)L * 2 * Ppad * 8 + (size_t)MFHE_DEC_SPLIT * L * Ppad * 6 * 8;
 }
 
 void balanced_digits(uint64_t x, int D, int8_t* out) {
@@ -1846,23 +1589,15 @@ static int launch_factored_inv(const ModGemmArgs& a, int L, hipStream_t s) {
         // decrypt fused (n = 64 rows: one workgroup per (y, l), 64 columns)
         if (a.log_n != 6 || a.P != 64u * 64u || Ppad != a.P || !a.dsk || !a.dlf || !a.dtw || !a.ditw || !a.dninv)
             return set_error(MFHE_EINVAL, "mod_gemm: the decrypt-fused inverse W-CRT needs n = 64 and the ring tables");
-        // MFHE_DEC_SPLIT workgroups per (row, limb), each a share of the 8 panels, the column sums finished after;
-        // with the coefficient-form key (MFHE_OPT_DEC_MM) the ring product on the matrix cores, DMM_G shares
+        // MFHE_DEC_SPLIT workgroups per (row, limb), each a share of the 8 panels, the column sums finished after
         constexpr int GS = MFHE_DEC_SPLIT;
         static_assert(GS == 1 || GS == 2 || GS == 4 || GS == 8, "the 8 panels split evenly");
-        const int G = a.dskc ? DMM_G : GS;
+        const int G = GS;
         f.dpart = f.cc + (size_t)L * Ppad * 2;
-        if (a.dskc) {
-            const dim3 gm(DMM_NSUB * 32 * L);
-            if (a.D == 5) hipLaunchKernelGGL(dec_mm_digitize_kernel<5>, gm, dim3(256), 0, s, f, Ppad, pc, L);
-            else hipLaunchKernelGGL(dec_mm_digitize_kernel<6>, gm, dim3(256), 0, s, f, Ppad, pc, L);
-            MFHE_CHECK_LAUNCH("dec_mm_digitize_kernel");
-        } else {
-            const dim3 gr(64, L, GS);
-            if (a.D == 5) hipLaunchKernelGGL(mfma_digitize_ifold_dec_kernel<5>, gr, dim3(256), 0, s, f, Ppad, pc);
-            else hipLaunchKernelGGL(mfma_digitize_ifold_dec_kernel<6>, gr, dim3(256), 0, s, f, Ppad, pc);
-            MFHE_CHECK_LAUNCH("mfma_digitize_ifold_dec_kernel");
-        }
+        const dim3 gr(64, L, GS);
+        if (a.D == 5) hipLaunchKernelGGL(mfma_digitize_ifold_dec_kernel<5>, gr, dim3(256), 0, s, f, Ppad, pc);
+        else hipLaunchKernelGGL(mfma_digitize_ifold_dec_kernel<6>, gr, dim3(256), 0, s, f, Ppad, pc);
+        MFHE_CHECK_LAUNCH("mfma_digitize_ifold_dec_kernel");
         if (G > 1) {
             hipLaunchKernelGGL(dec_colsum_kernel, dim3((Ppad + 255) / 256, L), dim3(256), 0, s, f, Ppad, G);
             MFHE_CHECK_LAUNCH("dec_colsum_kernel");
@@ -1932,26 +1667,17 @@ int launch_mod_gemm_pair(const ModGemmArgs& a, const ModGemmArgs& b, int L, hipS
     ModGemmArgs f[2] = {a, b};
     const dim3 gg(2 * Ppad / 64, FK / 64, 2 * L);
     if (inv) {
-        const bool mm = a.dskc && b.dskc;
-        const int G = mm ? DMM_G : MFHE_DEC_SPLIT;
+        const int G = MFHE_DEC_SPLIT;
         for (auto& x : f) {
             if (!x.dsk || !x.dlf || !x.dtw || !x.ditw || !x.dninv)
                 return set_error(MFHE_EINVAL, "mod_gemm: the decrypt-fused inverse W-CRT needs the ring tables");
             x.cc = (double*)(x.Bdig + (size_t)L * x.D * Ppad * MK);
             x.dpart = x.cc + (size_t)L * Ppad * 2;
         }
-        if (mm) {
-            const dim3 gm(DMM_NSUB * 64 * L);
-            if (a.D == 5) hipLaunchKernelGGL(dec_mm_digitize_pair_kernel<5>, gm, dim3(256), 0, s, f[0], f[1], Ppad, pc, L);
-            else hipLaunchKernelGGL(dec_mm_digitize_pair_kernel<6>, gm, dim3(256), 0, s, f[0], f[1], Ppad, pc, L);
-            MFHE_CHECK_LAUNCH("dec_mm_digitize_pair_kernel");
-        } else {
-            if (a.dskc || b.dskc) return set_error(MFHE_EINVAL, "mod_gemm pair: both or neither with the coefficient-form key");
-            const dim3 gr(64, 2 * L, G);
-            if (a.D == 5) hipLaunchKernelGGL(mfma_digitize_ifold_dec_pair_kernel<5>, gr, dim3(256), 0, s, f[0], f[1], Ppad, pc);
-            else hipLaunchKernelGGL(mfma_digitize_ifold_dec_pair_kernel<6>, gr, dim3(256), 0, s, f[0], f[1], Ppad, pc);
-            MFHE_CHECK_LAUNCH("mfma_digitize_ifold_dec_pair_kernel");
-        }
+        const dim3 gr(64, 2 * L, G);
+        if (a.D == 5) hipLaunchKernelGGL(mfma_digitize_ifold_dec_pair_kernel<5>, gr, dim3(256), 0, s, f[0], f[1], Ppad, pc);
+        else hipLaunchKernelGGL(mfma_digitize_ifold_dec_pair_kernel<6>, gr, dim3(256), 0, s, f[0], f[1], Ppad, pc);
+        MFHE_CHECK_LAUNCH("mfma_digitize_ifold_dec_pair_kernel");
         if (G > 1) {
             hipLaunchKernelGGL(dec_colsum_pair_kernel, dim3((Ppad + 255) / 256, 2 * L), dim3(256), 0, s, f[0], f[1], Ppad, G);
             MFHE_CHECK_LAUNCH("dec_colsum_pair_kernel");

@@ -68,8 +68,6 @@ struct ModGemmArgs {
     const uint64_t* dct = nullptr;
     uint64_t dtotal = 0;
     const uint64_t* dsk = nullptr;    // s [w][L][n], NTT form
-    const uint64_t* dskc = nullptr;   // s [w][L][n], coefficient form (canonical): set, the ring product runs on the
-                                      // matrix cores (gemm.hip dec_mm_digitize_kernel, MFHE_OPT_DEC_MM)
     const void* dlf = nullptr;        // LimbConst [L]
     const double* dtw = nullptr;      // X-NTT tables [L][n] (ph_f)
     const double* ditw = nullptr;

@@ -193,7 +193,6 @@ struct RingArgs {
     const double* itw;
     const double* ninv;      // [L]
     const uint64_t* sk;      // [w][L][n], NTT form
-    const uint64_t* skc = nullptr;   // the same in coefficient form (MFHE_OPT_DEC_MM), or null
     int L;
     uint64_t rows;           // 512 n L
 };
@@ -580,7 +579,6 @@ static int wcrt_args(mfhe_ctx* c, ModGemmArgs& a, const uint64_t* A, const uint6
         a.dct = B;
         a.dtotal = g.words;
         a.dsk = dec->sk;
-        a.dskc = dec->skc;
         a.dlf = dec->lf;
         a.dtw = dec->tw;
         a.ditw = dec->itw;
@@ -1087,18 +1085,6 @@ extern "C" int mfhe_decrypt_to_eval(mfhe_ctx* c, const uint64_t* ct, const uint6
     Bump b{(char*)c->ws};
     return decrypt_impl(c, ct, sk, out, (hipStream_t)s, &b);
 }
-// MFHE_OPT_DEC_MM: the key in coefficient form for the matrix-core ring product (gemm.hip dec_mm_digitize_kernel),
-// one inverse X-NTT of the 512 L rows per call into the workspace
-static int dec_key_coeff(mfhe_ctx* c, RingArgs& ra, Bump& b, hipStream_t s) {
-    if (!c->dec_mm) return MFHE_OK;
-    const Geo2 g = geo(c);
-    const size_t n = 512ull * g.L * g.n;
-    uint64_t* skc = b.get<uint64_t>(n);
-    MFHE_HIP(hipMemcpyAsync(skc, ra.sk, n * sizeof(uint64_t), hipMemcpyDeviceToDevice, s));
-    RC(mfhe_ntt_inv(c, skc, 512, 0, g.L, (mfhe_stream_t)s));
-    ra.skc = skc;
-    return MFHE_OK;
-}
 extern "C" int mfhe_decrypt_and_decode(mfhe_ctx* c, const uint64_t* cre, const uint64_t* cim, const uint64_t* sk,
                                        double* msg, mfhe_stream_t s) {
     RC(need_wcrt(c));
@@ -1109,7 +1095,6 @@ extern "C" int mfhe_decrypt_and_decode(mfhe_ctx* c, const uint64_t* cre, const u
     Bump b{(char*)c->ws};
     if (dec_fused_ok(c, g.logn)) {
         RingArgs ra = ring_args(c, sk, g.L, g.words / g.n);
-        RC(dec_key_coeff(c, ra, b, (hipStream_t)s));
         return decode_impl(c, cre, cim, msg, (hipStream_t)s, &b, &ra);
     }
     uint64_t* er = b.get<uint64_t>(g.words);
@@ -1165,7 +1150,6 @@ extern "C" int mfhe_decrypt_and_decode_sharded(mfhe_ctx* c, mfhe_ctx* call, mfhe
     Bump b{(char*)c->ws};
     if (dec_fused_ok(c, g.logn)) {
         RingArgs ra = ring_args(c, sk, g.L, g.words / g.n);
-        RC(dec_key_coeff(c, ra, b, (hipStream_t)s));
         return decode_sharded_impl(c, call, comm, mode, cre, cim, msg, (hipStream_t)s, &b, &ra);
     }
     uint64_t* er = b.get<uint64_t>(g.words);

@@ -124,7 +124,6 @@ struct mfhe_ctx {
     // has its own digit planes
     int he_streams = 3;
     int enc_a_direct = 1;         // MFHE_OPT_ENC_A_DIRECT
-    int dec_mm = 0;               // MFHE_OPT_DEC_MM
     hipStream_t he_side = nullptr;
     hipEvent_t he_fork = nullptr, he_join = nullptr;
     void* gemm_ws2 = nullptr;

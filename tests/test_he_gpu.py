@@ -510,16 +510,19 @@ def test_he_streams_encode_decode_identical(mfhe):
 
 
 @pytest.mark.parametrize("case", ["random", "extreme"])
-def test_dec_mm_matches_fp64_ring(mfhe, case):
-    """MFHE_OPT_DEC_MM: decrypt_and_decode's X ring product as i8-digit MFMA products against the key's negacyclic
-    matrix (gemm.hip dec_mm_digitize_kernel, the key brought to coefficient form by one inverse NTT) gives the same
-    doubles as the FP64 X-NTT row product (0), at the reference geometry, for random residues in every ciphertext
-    word and key word (not only keygen's keys) and for all-(q - 1) / zero words; with the decode's re / im on one
-    stream, as a pair launch (HE_STREAMS 2) and on the side stream (3)."""
+def test_decrypt_and_decode_stream_modes_agree_on_any_words(mfhe, case):
+    """decrypt_and_decode (the decrypt fused into the inverse W-CRT digitize) gives the same doubles with the decode's
+    re / im on one stream (HE_STREAMS 0), as a pair launch (2) and on the side stream (3), at the reference geometry,
+    for random residues in every ciphertext word and key word (not only keygen's keys) and for all-(q - 1) / zero
+    words.  MFHE_OPT_DEC_MM (the ring product on the matrix cores, r05: 2.4x slower) was removed in r06: only 0 is
+    accepted."""
     import torch
     ctx = mfhe.Context(RNS, 6, CONV)
     ctx.reserve_workspace()
-    assert ctx.get_option(mfhe.OPT_DEC_MM) in (0, 1)
+    assert ctx.get_option(mfhe.OPT_DEC_MM) == 0
+    ctx.set_option(mfhe.OPT_DEC_MM, 0)
+    with pytest.raises(mfhe.MfheError):
+        ctx.set_option(mfhe.OPT_DEC_MM, 1)
     rng = np.random.default_rng(11)
     q = np.array(RNS, np.uint64)[None, :, None]
     if case == "random":
@@ -534,15 +537,13 @@ def test_dec_mm_matches_fp64_ring(mfhe, case):
         sk = np.broadcast_to(q - 1, (512, 11, 64)).ravel().copy()
     dcre, dcim, dsk = (mfhe.to_device_u64(np.ascontiguousarray(x)) for x in (cre, cim, sk))
     out = {}
-    for mm in (0, 1):
-        ctx.set_option(mfhe.OPT_DEC_MM, mm)
-        for streams in (0, 2, 3):
-            ctx.set_option(mfhe.OPT_HE_STREAMS, streams)
-            res = torch.empty(512 * 4096 * 2, dtype=torch.float64, device="cuda")
-            ctx.decrypt_and_decode(dcre, dcim, dsk, res)
-            torch.cuda.synchronize()
-            out[(mm, streams)] = res.cpu().numpy()
-    ref = out[(0, 0)]
+    for streams in (0, 2, 3):
+        ctx.set_option(mfhe.OPT_HE_STREAMS, streams)
+        res = torch.empty(512 * 4096 * 2, dtype=torch.float64, device="cuda")
+        ctx.decrypt_and_decode(dcre, dcim, dsk, res)
+        torch.cuda.synchronize()
+        out[streams] = res.cpu().numpy()
+    ref = out[0]
     assert np.all(np.isfinite(ref))
     for k, v in out.items():
         np.testing.assert_array_equal(v, ref, err_msg=str(k))

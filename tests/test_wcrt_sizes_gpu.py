@@ -64,9 +64,14 @@ def test_wcrt_every_mode_every_size_matches_valu_and_oracle(mfhe, orc, bits):
     np.testing.assert_array_equal(ref_b, x)
     ref_v = np.zeros_like(v)
     orc.L.orc_wntt_forward_vector(P(v), P(ref_v), n, L, 512, P(U64(moduli)), orc.L.orc_he_V(h.h))
-    ref_b2 = np.zeros_like(x)
-    orc.L.orc_wntt_inverse_matrix(P(x), P(ref_b2), n, L, 512, P(U64(moduli)), orc.L.orc_he_VinvT(h.h))
-    dx, dv = mfhe.to_device_u64(x), mfhe.to_device_u64(v)
+    # the inverse of arbitrary canonical residues too, laid out poly-major [w n + y][limb][x] (its input layout), with
+    # the all-(q - 1) lane w = 0
+    xp = (rng.integers(0, 2 ** 63, (512 * n, L, n), dtype=np.uint64) % qv[None, :, None])
+    xp[:n] = (qv - np.uint64(1))[None, :, None]
+    xp = xp.ravel()
+    ref_b2 = np.zeros_like(xp)
+    orc.L.orc_wntt_inverse_matrix(P(xp), P(ref_b2), n, L, 512, P(U64(moduli)), orc.L.orc_he_VinvT(h.h))
+    dx, dv, dxp = mfhe.to_device_u64(x), mfhe.to_device_u64(v), mfhe.to_device_u64(xp)
     for mf, pipe in MODES:
         ctx.set_option(mfhe.OPT_WCRT_MFMA, mf)
         ctx.set_option(mfhe.OPT_WCRT_PIPE, pipe)
@@ -82,7 +87,7 @@ def test_wcrt_every_mode_every_size_matches_valu_and_oracle(mfhe, orc, bits):
         # the inverse of arbitrary residues too (not only of the forward's output)
         np.testing.assert_array_equal(mfhe.to_host_u64(b), x, err_msg="inv " + tag)
         b2 = torch.empty_like(dx)
-        ctx.wcrt_inv(dx, b2)
+        ctx.wcrt_inv(dxp, b2)
         torch.cuda.synchronize()
         np.testing.assert_array_equal(mfhe.to_host_u64(b2), ref_b2, err_msg="inv(random) " + tag)
         np.testing.assert_array_equal(mfhe.to_host_u64(vo), ref_v, err_msg="vector " + tag)

@@ -31,8 +31,6 @@ def main():
         ctx.set_option(18, int(os.environ["MFHE_HE_STREAMS"]))  # MFHE_OPT_HE_STREAMS
     if os.environ.get("MFHE_ENC_A_DIRECT"):
         ctx.set_option(19, int(os.environ["MFHE_ENC_A_DIRECT"]))  # MFHE_OPT_ENC_A_DIRECT
-    if os.environ.get("MFHE_DEC_MM"):
-        ctx.set_option(20, int(os.environ["MFHE_DEC_MM"]))  # MFHE_OPT_DEC_MM
     if os.environ.get("MFHE_CGEMM_MODE"):
         ctx.set_option(10, int(os.environ["MFHE_CGEMM_MODE"]))  # MFHE_OPT_CGEMM_MFMA
     t_ctx = time.perf_counter() - t0
