@@ -700,6 +700,10 @@ extern "C" int mfhe_ctx_set_option(mfhe_ctx* c, int opt, int64_t v) {
             if (v < 0 || v > 2) return set_error(MFHE_EINVAL, "trace split must be 0, 1 or 2");
             c->trace_split = (int)v;
             return MFHE_OK;
+        case MFHE_OPT_ENC_E_SMALL:
+            if (v < 0 || v > 1) return set_error(MFHE_EINVAL, "enc e small must be 0 or 1");
+            c->enc_e_small = (int)v;
+            return MFHE_OK;
         case MFHE_OPT_ENC_A_DIRECT:
             if (v < 0 || v > 1) return set_error(MFHE_EINVAL, "enc a direct must be 0 or 1");
             c->enc_a_direct = (int)v;
@@ -763,6 +767,7 @@ extern "C" int mfhe_ctx_get_option(const mfhe_ctx* c, int opt, int64_t* v) {
         case MFHE_OPT_NTT_U60: *v = c->ntt_u60 && c->u60_ok; return MFHE_OK;
         case MFHE_OPT_HE_STREAMS: *v = c->he_streams; return MFHE_OK;
         case MFHE_OPT_ENC_A_DIRECT: *v = c->enc_a_direct; return MFHE_OK;
+        case MFHE_OPT_ENC_E_SMALL: *v = c->enc_e_small; return MFHE_OK;
         case MFHE_OPT_DEC_MM: *v = 0; return MFHE_OK;
         default: return set_error(MFHE_EINVAL, "unknown option");
     }

@@ -1499,6 +1499,110 @@ static void launch_staged(int pipe, dim3 grid, hipStream_t s, const ModGemmArgs&
     hipLaunchKernelGGL((mod_gemm_mfma_lds_kernel<D, MODE>), grid, dim3(256), 0, s, f, Ppad, l0);
 }
 
+// ---- the W-CRT forward of a small signed operand (r06): the encrypt's Gaussian noise ----
+// The noise e is one small integer per (w, pos), the same in every limb: the reference's Box-Muller draw
+// (HE.cu:581-627) is 3.2 sqrt(-2 ln u1) cos(2 pi u2) with u1 >= 2^-53, so |e| <= 3.2 sqrt(106 ln 2) < 27.5 and e is its
+// own balanced base-256 digit.  The dense product V_l e then needs D_l x 1 digit pairs per MAC (acc_i = sum_k v_i e,
+// shift i only) against the factored forward's D_l x D_l at half the MACs: 2 D_l / D_l^2 = 0.4 of its MFMAs at
+// D_l = 5, with no digitize kernel (gaussian_i8_kernel writes the one plane, shared by every limb, in the GEMM's
+// k-panel-major layout) and no per-limb residue array.  Tile, LDS-DMA double buffer and lane maps as
+// mod_gemm_mfma_lds_kernel; per 64-k stage every thread issues DA + 1 DMAs (A's DA planes, then B's).  FP64 epilogue
+// (every q < 2^50): |acc_i| <= 512 * 128 * 28 < 2^21, z / y as in mfma_epilogue.
+template <int DA>
+__global__ __launch_bounds__(256, 2) void mod_gemm_mfma_smallb_kernel(ModGemmArgs a, const int8_t* __restrict__ b8,
+                                                                      uint32_t Ppad, int limb0) {
+    constexpr int KS = 64, PANEL = 64 * 32, PLANE = 2 * PANEL;   // one stage: two 32-k panels per plane
+    constexpr int STAGE = (DA + 1) * PLANE;                         // A's DA planes, then B's one
+    __shared__ __attribute__((aligned(16))) int8_t lds[2 * STAGE];
+    const int l = limb0 + blockIdx.z;
+    const int t = threadIdx.x, lane = t & 63, w = t >> 6;
+    const int r = lane & 31, h = lane >> 5;
+    const int mb = blockIdx.y * 64, pb = blockIdx.x * 64;
+    const int wm = (w & 1) * 32, wp = (w >> 1) * 32;
+    const int pp = t >> 7, li = t & 127;                            // this thread's k-panel of a stage and 16-B chunk
+    const int8_t* srcA = a.Adig + (uint64_t)l * a.adL + (uint64_t)mb * 32 + li * 16;
+    const int8_t* srcB = b8 + (uint64_t)pb * 32 + li * 16;
+    constexpr uint64_t kstrA = 512ull * 32, plA = 512ull * MK;      // A: k-panel / digit-plane strides
+    const uint64_t kstrB = (uint64_t)Ppad * 32;
+    const int wdst = pp * PANEL + ((li & ~63) * 16);                // this wave's LDS destination inside a plane
+    auto issue = [&](int s, int buf) {
+        int8_t* st = lds + buf * STAGE + wdst;
+        const uint64_t kp = (uint64_t)(2 * s + pp);
+#pragma unroll
+        for (int i = 0; i < DA; ++i)
+            __builtin_amdgcn_global_load_lds((const void*)(srcA + i * plA + kp * kstrA), (lds_ptr_t)(st + i * PLANE), 16,
+                                             0, 0);
+        __builtin_amdgcn_global_load_lds((const void*)(srcB + kp * kstrB), (lds_ptr_t)(st + DA * PLANE), 16, 0, 0);
+    };
+    v16i acc[DA];
+#pragma unroll
+    for (int i = 0; i < DA; ++i) acc[i] = v16i{0};
+    issue(0, 0);
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+    for (int s = 0; s < MK / KS; ++s) {
+        const int buf = s & 1;
+        if (s + 1 < MK / KS) issue(s + 1, buf ^ 1);   // buf ^ 1's last readers all passed the previous barrier
+        const int8_t* st = lds + buf * STAGE;
+#pragma unroll
+        for (int q = 0; q < 2; ++q) {
+            const v4i bv = *(const v4i*)(st + DA * PLANE + q * PANEL + (wp + r) * 32 + 16 * h);
+#pragma unroll
+            for (int i = 0; i < DA; ++i) {
+                const v4i av = *(const v4i*)(st + i * PLANE + q * PANEL + (wm + r) * 32 + 16 * h);
+                acc[i] = __builtin_amdgcn_mfma_i32_32x32x32_i8(av, bv, acc[i], 0, 0, 0);
+            }
+        }
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // this wave's DMAs into buf ^ 1 have landed
+        __syncthreads();
+    }
+    // FP64 epilogue: C = sum_i acc_i 256^i mod q, canonical
+    typedef const __attribute__((address_space(4))) double* cdp_t;
+    const cdp_t ep = (cdp_t)(a.epi + (uint64_t)l * 8);
+    LimbConst lc;
+    lc.qf = ep[0];
+    lc.qinv = ep[1];
+    const ArithF64 ar(lc);
+    const double c32[3] = {ep[2], ep[3], ep[4]};
+    const uint32_t col = pb + wp + r;
+    if (col >= a.P) return;
+    uint64_t* Cl = a.C + (uint64_t)l * a.cL + (uint64_t)(col >> a.log_n) * a.scY + (col & ((1u << a.log_n) - 1));
+    constexpr int NZ = (DA + 1) / 2, NY = (NZ + 1) / 2;
+#pragma unroll
+    for (int reg = 0; reg < 16; ++reg) {
+        const int row = mb + wm + (reg & 3) + 8 * (reg >> 2) + 4 * h;
+        double z[NZ];
+#pragma unroll
+        for (int u = 0; u < NZ; ++u)
+            z[u] = 2 * u + 1 < DA ? __fma_rn(256.0, (double)acc[2 * u + 1][reg], (double)acc[2 * u][reg])
+                                  : (double)acc[2 * u][reg];
+        double v = 0.0;
+#pragma unroll
+        for (int u = 0; u < NY; ++u) {
+            const double y = 2 * u + 1 < NZ ? __fma_rn(65536.0, z[2 * u + 1], z[2 * u]) : z[2 * u];
+            v += u == 0 ? y : ar.mulmod(y, c32[u - 1]);
+        }
+        Cl[(uint64_t)row * a.scM] = ar.canon(v);
+    }
+}
+
+int launch_mod_gemm_smallb(const ModGemmArgs& a, const int8_t* b8, int L, hipStream_t s) {
+    if (!a.Adig || !a.epi || a.M != 512 || a.K != MK || a.fold || a.ifold || a.D < 5 || a.D > 6 || a.adL == 0)
+        return set_error(MFHE_EINVAL, "mod_gemm_smallb: needs the dense per-limb V planes (5 or 6 digits) and the FP64 epilogue");
+    const uint32_t Ppad = (a.P + 63) / 64 * 64;
+    for (int l0 = 0; l0 < L;) {
+        const int d = a.limbD ? std::max(a.limbD[l0], 5) : a.D;
+        int l1 = l0 + 1;
+        while (l1 < L && (a.limbD ? std::max(a.limbD[l1], 5) : a.D) == d) ++l1;
+        const dim3 grid(Ppad / 64, 512 / 64, l1 - l0);
+        if (d == 5) hipLaunchKernelGGL(mod_gemm_mfma_smallb_kernel<5>, grid, dim3(256), 0, s, a, b8, Ppad, l0);
+        else hipLaunchKernelGGL(mod_gemm_mfma_smallb_kernel<6>, grid, dim3(256), 0, s, a, b8, Ppad, l0);
+        MFHE_CHECK_LAUNCH("mod_gemm_mfma_smallb_kernel");
+        l0 = l1;
+    }
+    return MFHE_OK;
+}
+
 size_t mod_gemm_mfma_ws(uint32_t P, int L, int D) {
     const uint64_t Ppad = ((uint64_t)P + 63) / 64 * 64;
     // digit planes, then the factored d0 / (c0, c1), then the split decrypt-fused digitize's column partials

@@ -101,6 +101,9 @@ struct CGemmArgs {
 };
 
 int launch_mod_gemm(const ModGemmArgs& a, int L, hipStream_t s);
+// the dense W-CRT forward of one small signed int8 operand shared by every limb (the encrypt's Gaussian noise, |e| <=
+// 27): b8 is its one digit plane [K/32][Ppad][32]; a as launch_mod_gemm's dense MFMA arguments (gemm.hip)
+int launch_mod_gemm_smallb(const ModGemmArgs& a, const int8_t* b8, int L, hipStream_t s);
 // two independent W-CRT transforms of the same shape as one launch per step (gemm.hip; he.hip encode / decode)
 int launch_mod_gemm_pair(const ModGemmArgs& a, const ModGemmArgs& b, int L, hipStream_t s);
 int launch_cgemm(const CGemmArgs& a, int batch, hipStream_t s);

@@ -124,6 +124,32 @@ __global__ void gaussian_compact_kernel(double* e, int log_n, uint64_t total) {
     e[idx] = (double)llround(z);
 }
 
+// The same draw once more, written as the one signed digit of e in the dense W-CRT GEMM's B layout (k-panel-major
+// [512 / 32][P][32] bytes, k = w, p = pos; gemm.hip mod_gemm_mfma_smallb_kernel), shared by every limb: |e| <= 27
+// (u1 >= 2^-53), so the int8 holds e exactly.  One thread per 4 consecutive k of one position (a 4-byte store), the
+// 8 threads of a position's 32-k panel row adjacent: every wave writes 2 KiB contiguous.
+__global__ void gaussian_i8_kernel(int8_t* __restrict__ b8, int log_n, uint32_t P) {
+    const uint64_t idx = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x;   // (panel, pos, k group of 4)
+    if (idx >= 128ull * P) return;
+    const uint64_t row = idx >> 3;                                          // panel * P + pos
+    const uint32_t pos = (uint32_t)(row % P), k0 = (uint32_t)(row / P) * 32 + (uint32_t)(idx & 7) * 4;
+    const uint64_t n2 = 1ull << (2 * log_n);
+    uint32_t word = 0;
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+        const uint64_t w = k0 + j;
+        const uint64_t r1 = splitmix64(0xD6E8FEB86659FD93ULL ^ (w * n2 + pos));
+        const uint64_t r2 = splitmix64(r1);
+        const double inv53 = 1.0 / 9007199254740992.0;
+        const double u1 = ((double)(r1 >> 11) + 1.0) * inv53;
+        const double u2 = ((double)(r2 >> 11) + 1.0) * inv53;
+        const double mag = 3.2 * sqrt(-2.0 * log(u1));
+        const double z = mag * cos(6.283185307179586 * u2);
+        word |= (uint32_t)(uint8_t)(int8_t)llround(z) << (8 * j);
+    }
+    *(uint32_t*)(b8 + row * 32 + (k0 & 31)) = word;
+}
+
 // ---------------- ring ops (poly-major [phi*n][L][n]) ----------------
 // pointwise_mul_s_kernel HE.cu:509-531: t = a * s[w][l][x], w = poly / n.  The reference reduces with
 // an __int128 % per element (a software division here too); this uses the exact FP64 modmul of the NTT
@@ -836,12 +862,28 @@ static int encrypt_impl(mfhe_ctx* c, const uint64_t* m_re, const uint64_t* m_im,
         if (a_mm) RC(wcrt_args(c, aa, c->d_wV, ap, false, ct_re + W, WOut::Matrix, false, 2, nullptr, 1, nullptr, 0,
                                m_im ? ct_im + W : nullptr));
         else RC(wcrt_args(c, aa, c->d_wV, ap, false, aev, WOut::Poly, false, 2));
-        RC(wcrt_args(c, ae, c->d_wV, ep, false, eev, WOut::Poly, false, 3, (const double*)ep, 1, nullptr, pair ? 1 : 0));
-        if (!pair) RC(launch_mod_gemm(aa, g.L, s));
-        hipLaunchKernelGGL(gaussian_compact_kernel, g1(W / g.L), dim3(256), 0, s, (double*)ep, g.logn, W / g.L);
-        MFHE_CHECK_LAUNCH("gaussian_compact_kernel");
-        if (pair) RC(launch_mod_gemm_pair(aa, ae, g.L, s));
-        else RC(launch_mod_gemm(ae, g.L, s));
+        // the noise: its W-CRT forward as the dense product with its one signed digit (MFHE_OPT_ENC_E_SMALL, gemm.hip
+        // mod_gemm_mfma_smallb_kernel) where the dense V planes have 5-6 digits; else factored from its residues
+        const bool e_small = c->enc_e_small && !pair && c->d_wVdig && c->wD >= 5 && c->wD <= 6 && g.n2 % 64 == 0;
+        if (e_small) {
+            RC(wcrt_args(c, ae, c->d_wV, ep, false, eev, WOut::Poly, false));
+            ae.Adig = c->d_wVdig;   // the dense V planes (use_mfma chose the factored ones)
+            ae.adL = (uint64_t)c->wD * 512 * 512;
+            ae.fold = nullptr;
+            RC(launch_mod_gemm(aa, g.L, s));
+            int8_t* b8 = (int8_t*)ep;   // 512 x n^2 bytes, inside the unused residue buffer
+            hipLaunchKernelGGL(gaussian_i8_kernel, g1(128ull * g.n2), dim3(256), 0, s, b8, g.logn, (uint32_t)g.n2);
+            MFHE_CHECK_LAUNCH("gaussian_i8_kernel");
+            RC(launch_mod_gemm_smallb(ae, b8, g.L, s));
+        } else {
+            RC(wcrt_args(c, ae, c->d_wV, ep, false, eev, WOut::Poly, false, 3, (const double*)ep, 1, nullptr,
+                         pair ? 1 : 0));
+            if (!pair) RC(launch_mod_gemm(aa, g.L, s));
+            hipLaunchKernelGGL(gaussian_compact_kernel, g1(W / g.L), dim3(256), 0, s, (double*)ep, g.logn, W / g.L);
+            MFHE_CHECK_LAUNCH("gaussian_compact_kernel");
+            if (pair) RC(launch_mod_gemm_pair(aa, ae, g.L, s));
+            else RC(launch_mod_gemm(ae, g.L, s));
+        }
     } else {
         hipLaunchKernelGGL(uniform_kernel, g1(W), dim3(256), 0, s, ap, c->d_rns_mu, g.L, g.logn, W, c->limb_base,
                            c->limbs_total ? c->limbs_total : g.L);

@@ -124,6 +124,7 @@ struct mfhe_ctx {
     // has its own digit planes
     int he_streams = 3;
     int enc_a_direct = 1;         // MFHE_OPT_ENC_A_DIRECT
+    int enc_e_small = 1;          // MFHE_OPT_ENC_E_SMALL
     hipStream_t he_side = nullptr;
     hipEvent_t he_fork = nullptr, he_join = nullptr;
     void* gemm_ws2 = nullptr;

@@ -40,6 +40,7 @@ OPT_NTT_PLAN_EFFECTIVE = 15   # read-only: 4 pipelined single pass (2^14 FP64), 
 OPT_NTT_U60 = 17              # U64 NTTs with every modulus < 2^60: 1 = lazy U60 schedules (default), 0 = Harvey
 OPT_HE_STREAMS = 18           # encode / encrypt_pair / decrypt_and_decode re/im chains: 3 = encode pairs + decode side stream (default), 2 = pairs, 1 = side stream, 0 = one stream
 OPT_ENC_A_DIRECT = 19         # encrypt (fused ring): 1 = the GEMM writes a into both ciphertexts (default), 0 = ring kernel copies it
+OPT_ENC_E_SMALL = 21          # encrypt: 1 = the noise's W-CRT as the dense product with its one digit (default), 0 = factored
 OPT_DEC_MM = 20               # removed in r06 (the decrypt's ring product on the matrix cores): only 0 accepted; was FP64 X-NTT rows (default)
 COMM_ID_BYTES = 128
 

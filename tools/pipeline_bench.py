@@ -31,6 +31,8 @@ def main():
         ctx.set_option(18, int(os.environ["MFHE_HE_STREAMS"]))  # MFHE_OPT_HE_STREAMS
     if os.environ.get("MFHE_ENC_A_DIRECT"):
         ctx.set_option(19, int(os.environ["MFHE_ENC_A_DIRECT"]))  # MFHE_OPT_ENC_A_DIRECT
+    if os.environ.get("MFHE_ENC_E_SMALL"):
+        ctx.set_option(21, int(os.environ["MFHE_ENC_E_SMALL"]))  # MFHE_OPT_ENC_E_SMALL
     if os.environ.get("MFHE_CGEMM_MODE"):
         ctx.set_option(10, int(os.environ["MFHE_CGEMM_MODE"]))  # MFHE_OPT_CGEMM_MFMA
     t_ctx = time.perf_counter() - t0
