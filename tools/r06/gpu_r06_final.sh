@@ -3,7 +3,7 @@
 # headline kernel trace + PMC traffic (tools/profile_headline.sh), the pipeline kernel trace and the U64 line's
 # kernel trace (U60 vs Harvey).  Each GPU step has its own limit; the chain stops at the first failure.
 set -o pipefail
-O=gpurun_out/r06final
+O=gpurun_out/${R06TAG:-r06final}
 ROOT=${GRAFT_REPO_ROOT:-$(pwd)}
 mkdir -p $O
 export PYTHONUNBUFFERED=1
@@ -14,7 +14,7 @@ timeout -k 10 300 python -u -c "import __graft_entry__ as g; g.smoke()" > $O/smo
 tail -1 $O/smoke.log
 timeout -k 10 600 python -u bench.py > $O/bench_default.json 2> $O/bench_default.err || { echo "bench rc=$?"; tail -20 $O/bench_default.err; exit 3; }
 python3 -c "import json; d=json.load(open('$O/bench_default.json')); print(d['value'], d['roofline']['frac'], d.get('reference_geometry_pipeline',{}).get('ms'))"
-bash tools/profile_headline.sh r06final_prof || { echo "profile_headline rc=$?"; exit 4; }
+bash tools/profile_headline.sh ${R06TAG:-r06final}_prof || { echo "profile_headline rc=$?"; exit 4; }
 cd /tmp && export TMPDIR=/tmp
 timeout -k 10 300 rocprofv3 --kernel-trace --stats -d $ROOT/$O/pipe_prof -o run --output-format csv -- \
     python3 $ROOT/tools/pipeline_bench.py 10 > $ROOT/$O/pipe_prof.log 2>&1 || { echo "pipe prof rc=$?"; tail -10 $ROOT/$O/pipe_prof.log; exit 5; }
