@@ -1505,20 +1505,21 @@ static void launch_staged(int pipe, dim3 grid, hipStream_t s, const ModGemmArgs&
 // own balanced base-256 digit.  The dense product V_l e then needs D_l x 1 digit pairs per MAC (acc_i = sum_k v_i e,
 // shift i only) against the factored forward's D_l x D_l at half the MACs: 2 D_l / D_l^2 = 0.4 of its MFMAs at
 // D_l = 5, with no digitize kernel (gaussian_i8_kernel writes the one plane, shared by every limb, in the GEMM's
-// k-panel-major layout) and no per-limb residue array.  Tile, LDS-DMA double buffer and lane maps as
-// mod_gemm_mfma_lds_kernel; per 64-k stage every thread issues DA + 1 DMAs (A's DA planes, then B's).  FP64 epilogue
-// (every q < 2^50): |acc_i| <= 512 * 128 * 28 < 2^21, z / y as in mfma_epilogue.
-template <int DA>
-__global__ __launch_bounds__(256, 2) void mod_gemm_mfma_smallb_kernel(ModGemmArgs a, const int8_t* __restrict__ b8,
-                                                                      uint32_t Ppad, int limb0) {
-    constexpr int KS = 64, PANEL = 64 * 32, PLANE = 2 * PANEL;   // one stage: two 32-k panels per plane
-    constexpr int STAGE = (DA + 1) * PLANE;                         // A's DA planes, then B's one
-    __shared__ __attribute__((aligned(16))) int8_t lds[2 * STAGE];
-    const int l = limb0 + blockIdx.z;
+// k-panel-major layout) and no per-limb residue array.
+// Tile 64 rows x 64 NC columns, four waves as 2 x 2 (each 32 rows x 32 NC columns, NC accumulator sets per digit);
+// 64-k LDS-DMA stages, double-buffered, per stage every thread issues DA + NC DMAs (A's DA planes, then B's NC).
+// A's DA planes are the bulk of a stage, so NC = 2 halves the A bytes per MAC (r06 counters at NC = 1: MFMA busy
+// 0.21, waits 0.54 of wave cycles; a third stage buffer was slower).  FP64 epilogue (every q < 2^50):
+// |acc_i| <= 512 * 128 * 28 < 2^21, z / y as in mfma_epilogue.
+template <int DA, int NC>
+__device__ __forceinline__ void smallb_mma(const ModGemmArgs& a, const int8_t* __restrict__ b8, uint32_t Ppad, int l,
+                                           int mb, int pb, int8_t* lds, v16i (&acc)[NC][DA]) {
+    constexpr int KS = 64, PANEL = 64 * 32, PLANE = 2 * PANEL;   // one stage: two 32-k panels per 64-row plane
+    constexpr int STAGE = (DA + NC) * PLANE;                        // A's DA planes, then B's NC (64 columns each)
+    constexpr int NS = MK / KS;
     const int t = threadIdx.x, lane = t & 63, w = t >> 6;
     const int r = lane & 31, h = lane >> 5;
-    const int mb = blockIdx.y * 64, pb = blockIdx.x * 64;
-    const int wm = (w & 1) * 32, wp = (w >> 1) * 32;
+    const int wm = (w & 1) * 32, wp = (w >> 1) * 32 * NC;          // this wave's rows / first column in the tile
     const int pp = t >> 7, li = t & 127;                            // this thread's k-panel of a stage and 16-B chunk
     const int8_t* srcA = a.Adig + (uint64_t)l * a.adL + (uint64_t)mb * 32 + li * 16;
     const int8_t* srcB = b8 + (uint64_t)pb * 32 + li * 16;
@@ -1532,31 +1533,70 @@ __global__ __launch_bounds__(256, 2) void mod_gemm_mfma_smallb_kernel(ModGemmArg
         for (int i = 0; i < DA; ++i)
             __builtin_amdgcn_global_load_lds((const void*)(srcA + i * plA + kp * kstrA), (lds_ptr_t)(st + i * PLANE), 16,
                                              0, 0);
-        __builtin_amdgcn_global_load_lds((const void*)(srcB + kp * kstrB), (lds_ptr_t)(st + DA * PLANE), 16, 0, 0);
-    };
-    v16i acc[DA];
 #pragma unroll
-    for (int i = 0; i < DA; ++i) acc[i] = v16i{0};
+        for (int c = 0; c < NC; ++c)
+            __builtin_amdgcn_global_load_lds((const void*)(srcB + c * 64 * 32 + kp * kstrB),
+                                             (lds_ptr_t)(st + (DA + c) * PLANE), 16, 0, 0);
+    };
+#pragma unroll
+    for (int c = 0; c < NC; ++c)
+#pragma unroll
+        for (int i = 0; i < DA; ++i) acc[c][i] = v16i{0};
     issue(0, 0);
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __syncthreads();
-    for (int s = 0; s < MK / KS; ++s) {
+#pragma unroll 1
+    for (int s = 0; s < NS; ++s) {
         const int buf = s & 1;
-        if (s + 1 < MK / KS) issue(s + 1, buf ^ 1);   // buf ^ 1's last readers all passed the previous barrier
+        if (s + 1 < NS) issue(s + 1, buf ^ 1);   // buf ^ 1's last readers all passed the previous barrier
         const int8_t* st = lds + buf * STAGE;
 #pragma unroll
         for (int q = 0; q < 2; ++q) {
-            const v4i bv = *(const v4i*)(st + DA * PLANE + q * PANEL + (wp + r) * 32 + 16 * h);
+            v4i bv[NC];
+#pragma unroll
+            for (int c = 0; c < NC; ++c) {
+                const int tc = wp + 32 * c;   // tile column of this 32-column block: 64-column plane tc / 64
+                bv[c] = *(const v4i*)(st + (DA + tc / 64) * PLANE + q * PANEL + (tc % 64 + r) * 32 + 16 * h);
+            }
 #pragma unroll
             for (int i = 0; i < DA; ++i) {
                 const v4i av = *(const v4i*)(st + i * PLANE + q * PANEL + (wm + r) * 32 + 16 * h);
-                acc[i] = __builtin_amdgcn_mfma_i32_32x32x32_i8(av, bv, acc[i], 0, 0, 0);
+#pragma unroll
+                for (int c = 0; c < NC; ++c) acc[c][i] = __builtin_amdgcn_mfma_i32_32x32x32_i8(av, bv[c], acc[c][i], 0, 0, 0);
             }
         }
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // this wave's DMAs into buf ^ 1 have landed
         __syncthreads();
     }
-    // FP64 epilogue: C = sum_i acc_i 256^i mod q, canonical
+}
+
+// C = sum_i acc_i 256^i mod q, canonical, for accumulator register `reg` (FP64: z / y as in mfma_epilogue)
+template <int DA>
+__device__ __forceinline__ uint64_t smallb_value(const ArithF64& ar, const double (&c32)[3], const v16i (&acc)[DA],
+                                                 int reg) {
+    constexpr int NZ = (DA + 1) / 2, NY = (NZ + 1) / 2;
+    double z[NZ];
+#pragma unroll
+    for (int u = 0; u < NZ; ++u)
+        z[u] = 2 * u + 1 < DA ? __fma_rn(256.0, (double)acc[2 * u + 1][reg], (double)acc[2 * u][reg])
+                              : (double)acc[2 * u][reg];
+    double v = 0.0;
+#pragma unroll
+    for (int u = 0; u < NY; ++u) {
+        const double y = 2 * u + 1 < NZ ? __fma_rn(65536.0, z[2 * u + 1], z[2 * u]) : z[2 * u];
+        v += u == 0 ? y : ar.mulmod(y, c32[u - 1]);
+    }
+    return ar.canon(v);
+}
+
+template <int DA, int NC>
+__global__ __launch_bounds__(256, 2) void mod_gemm_mfma_smallb_kernel(ModGemmArgs a, const int8_t* __restrict__ b8,
+                                                                      uint32_t Ppad, int limb0) {
+    __shared__ __attribute__((aligned(16))) int8_t lds[2 * (DA + NC) * 64 * 64];
+    const int l = limb0 + blockIdx.z;
+    const int mb = blockIdx.y * 64, pb = blockIdx.x * 64 * NC;
+    v16i acc[NC][DA];
+    smallb_mma<DA, NC>(a, b8, Ppad, l, mb, pb, lds, acc);
     typedef const __attribute__((address_space(4))) double* cdp_t;
     const cdp_t ep = (cdp_t)(a.epi + (uint64_t)l * 8);
     LimbConst lc;
@@ -1564,39 +1604,35 @@ __global__ __launch_bounds__(256, 2) void mod_gemm_mfma_smallb_kernel(ModGemmArg
     lc.qinv = ep[1];
     const ArithF64 ar(lc);
     const double c32[3] = {ep[2], ep[3], ep[4]};
-    const uint32_t col = pb + wp + r;
-    if (col >= a.P) return;
-    uint64_t* Cl = a.C + (uint64_t)l * a.cL + (uint64_t)(col >> a.log_n) * a.scY + (col & ((1u << a.log_n) - 1));
-    constexpr int NZ = (DA + 1) / 2, NY = (NZ + 1) / 2;
+    const int lane = threadIdx.x & 63, w = threadIdx.x >> 6, r = lane & 31, h = lane >> 5;
+    const int wm = (w & 1) * 32, wp = (w >> 1) * 32 * NC;
 #pragma unroll
-    for (int reg = 0; reg < 16; ++reg) {
-        const int row = mb + wm + (reg & 3) + 8 * (reg >> 2) + 4 * h;
-        double z[NZ];
+    for (int c = 0; c < NC; ++c) {
+        const uint32_t col = pb + wp + 32 * c + r;
+        if (col >= a.P) continue;
+        uint64_t* Cl = a.C + (uint64_t)l * a.cL + (uint64_t)(col >> a.log_n) * a.scY + (col & ((1u << a.log_n) - 1));
 #pragma unroll
-        for (int u = 0; u < NZ; ++u)
-            z[u] = 2 * u + 1 < DA ? __fma_rn(256.0, (double)acc[2 * u + 1][reg], (double)acc[2 * u][reg])
-                                  : (double)acc[2 * u][reg];
-        double v = 0.0;
-#pragma unroll
-        for (int u = 0; u < NY; ++u) {
-            const double y = 2 * u + 1 < NZ ? __fma_rn(65536.0, z[2 * u + 1], z[2 * u]) : z[2 * u];
-            v += u == 0 ? y : ar.mulmod(y, c32[u - 1]);
-        }
-        Cl[(uint64_t)row * a.scM] = ar.canon(v);
+        for (int reg = 0; reg < 16; ++reg)
+            Cl[(uint64_t)(mb + wm + (reg & 3) + 8 * (reg >> 2) + 4 * h) * a.scM] = smallb_value<DA>(ar, c32, acc[c], reg);
     }
 }
 
+// b8: [512 / 32][Ppad][32] with Ppad = P rounded up to 64; the two-block tile (NC = 2) needs Ppad % 128 == 0 so that
+// no stage reads past the plane
 int launch_mod_gemm_smallb(const ModGemmArgs& a, const int8_t* b8, int L, hipStream_t s) {
     if (!a.Adig || !a.epi || a.M != 512 || a.K != MK || a.fold || a.ifold || a.D < 5 || a.D > 6 || a.adL == 0)
         return set_error(MFHE_EINVAL, "mod_gemm_smallb: needs the dense per-limb V planes (5 or 6 digits) and the FP64 epilogue");
     const uint32_t Ppad = (a.P + 63) / 64 * 64;
+    const int nc = Ppad % 128 == 0 ? 2 : 1;
     for (int l0 = 0; l0 < L;) {
         const int d = a.limbD ? std::max(a.limbD[l0], 5) : a.D;
         int l1 = l0 + 1;
         while (l1 < L && (a.limbD ? std::max(a.limbD[l1], 5) : a.D) == d) ++l1;
-        const dim3 grid(Ppad / 64, 512 / 64, l1 - l0);
-        if (d == 5) hipLaunchKernelGGL(mod_gemm_mfma_smallb_kernel<5>, grid, dim3(256), 0, s, a, b8, Ppad, l0);
-        else hipLaunchKernelGGL(mod_gemm_mfma_smallb_kernel<6>, grid, dim3(256), 0, s, a, b8, Ppad, l0);
+        const dim3 grid(Ppad / (64 * nc), 512 / 64, l1 - l0);
+        if (d == 5 && nc == 2) hipLaunchKernelGGL((mod_gemm_mfma_smallb_kernel<5, 2>), grid, dim3(256), 0, s, a, b8, Ppad, l0);
+        else if (d == 5) hipLaunchKernelGGL((mod_gemm_mfma_smallb_kernel<5, 1>), grid, dim3(256), 0, s, a, b8, Ppad, l0);
+        else if (nc == 2) hipLaunchKernelGGL((mod_gemm_mfma_smallb_kernel<6, 2>), grid, dim3(256), 0, s, a, b8, Ppad, l0);
+        else hipLaunchKernelGGL((mod_gemm_mfma_smallb_kernel<6, 1>), grid, dim3(256), 0, s, a, b8, Ppad, l0);
         MFHE_CHECK_LAUNCH("mod_gemm_mfma_smallb_kernel");
         l0 = l1;
     }

@@ -336,13 +336,15 @@ def _encrypt_decrypt_vs_oracle(mfhe, orc, n, ctx, h, moduli):
     np.testing.assert_array_equal(mfhe.to_host_u64(ev), h.decrypt_to_eval(gre, sk_ref))
 
 
-@pytest.mark.parametrize("n,L", [(8, 11), (16, 3), (64, 11), (64, 1), (8, 16)])
+@pytest.mark.parametrize("n,L", [(8, 11), (16, 3), (64, 11), (64, 1), (8, 16), (64, 16)])
 def test_encrypt_noise_small_operand_gemm_matches_factored(mfhe, n, L):
-    """MFHE_OPT_ENC_E_SMALL (r06, default 1): the encrypt's Gaussian noise enters its W-CRT forward as the dense
-    product with its one signed digit (gemm.hip mod_gemm_mfma_smallb_kernel; |e| <= 27 from the Box-Muller bound) and
-    is never written as residues; 0 takes the factored forward of its residues.  The ciphertexts are identical, for
-    limbs of 5 and 6 digits (the reference moduli: limb 0 has 44 bits), one limb, and BASELINE C4's 16 x 35-bit
-    primes; and identical to the pair launch (HE_STREAMS 2), which keeps the factored form."""
+    """MFHE_OPT_ENC_E_SMALL (r06): the encrypt's Gaussian noise enters its W-CRT forward as the dense product with its
+    one signed digit (|e| <= 27 from the Box-Muller bound) and is never written as residues.  1 (default): gemm.hip
+    mod_gemm_mfma_smallb_kernel, 64 x 128 tiles where n^2 % 128 == 0, else 64 x 64; 0: the factored forward of its
+    residues.  The ciphertexts are identical, for limbs of 5 and 6 digits (the reference moduli: limb 0 has 44
+    bits), one limb, and BASELINE C4's 16 x 35-bit primes; with a through both ciphertexts (ENC_A_DIRECT 1) or through
+    the poly-major buffer (0); for encrypt_pair and encrypt; and identical to the pair launch (HE_STREAMS 2), which
+    keeps the factored form."""
     import torch
     from bench import gen_moduli
     moduli = RNS[:L] if L <= 11 else gen_moduli(35, 197376, L)
@@ -355,18 +357,27 @@ def test_encrypt_noise_small_operand_gemm_matches_factored(mfhe, n, L):
                   for _ in range(2))
     sk = torch.empty(512 * L * n, dtype=torch.int64, device="cuda")
     ctx.keygen(sk)
-    out = {}
-    for small, streams in ((1, 3), (0, 3), (1, 2), (1, 0)):
+    out, single = {}, {}
+    for small, streams, adirect in ((1, 3, 1), (0, 3, 1), (1, 3, 0), (1, 2, 1), (1, 0, 1)):
         ctx.set_option(mfhe.OPT_ENC_E_SMALL, small)
         ctx.set_option(mfhe.OPT_HE_STREAMS, streams)
+        ctx.set_option(mfhe.OPT_ENC_A_DIRECT, adirect)
         cre = torch.full((2 * words,), -1, dtype=torch.int64, device="cuda")
         cim = torch.full_like(cre, -1)
         ctx.encrypt_pair(m_re, m_im, sk, cre, cim)
         torch.cuda.synchronize()
-        out[(small, streams)] = (mfhe.to_host_u64(cre), mfhe.to_host_u64(cim))
+        out[(small, streams, adirect)] = (mfhe.to_host_u64(cre), mfhe.to_host_u64(cim))
+        if streams == 3 and adirect == 1:
+            ct = torch.full((2 * words,), -1, dtype=torch.int64, device="cuda")
+            ctx.encrypt(m_re, sk, ct)
+            torch.cuda.synchronize()
+            single[small] = mfhe.to_host_u64(ct)
+    ref = out[(0, 3, 1)]
     for key, (a, b) in out.items():
-        np.testing.assert_array_equal(a, out[(0, 3)][0], err_msg=str(key))
-        np.testing.assert_array_equal(b, out[(0, 3)][1], err_msg=str(key))
+        np.testing.assert_array_equal(a, ref[0], err_msg=str(key))
+        np.testing.assert_array_equal(b, ref[1], err_msg=str(key))
+    for small, ct in single.items():
+        np.testing.assert_array_equal(ct, single[0], err_msg=f"encrypt, option {small}")
     with pytest.raises(mfhe.MfheError):
         ctx.set_option(mfhe.OPT_ENC_E_SMALL, 2)
     ctx.close()
