@@ -20,8 +20,13 @@ namespace mfhe {
 // round trips.  T = n/4 lanes per row, lane j holds coefficients 4j..4j+3; butterflies at distance
 // t >= 4 pair lane j with lane j ^ (t/4), each lane of the pair computing two of the four butterflies;
 // t = 1, 2 stay in the lane.
-// FP64 exact modmul (ntt_arith.hpp); bounds: |mulmod| <= 1.5 q, forward values are re-centred every two
-// stages (|v| <= 2 q into a mulmod), inverse X every stage (|u - v| <= 3 q), q < 2^50.
+// FP64 exact modmul (ntt_arith.hpp), q < 2^50.  Bounds (r06): a mulmod of |v| <= 4q by a centred |w| <= q/2 is
+// within q (|hi - k q| <= q/2 + |hi| 2^-53 <= 0.75 q, |lo| <= ulp(hi) / 2 <= q / 4) and needs |v w / q| < 2^51, i.e.
+// |v| <= 4q.  Forward: the input is canonical (< q) and each CT stage adds at most q, so the fourth stage's v is
+// <= 4q; one centred reduction after stage 4 (r05: after every second stage); stages 5-6 end <= 2.5q, the input of
+// the product with s.  Inverse: X is left unreduced on every other stage starting with the first (as
+// ArithF64::gs_lazy: a lazy stage's inputs are <= q, so its X < 2q and the next stage's |u - v| < 4q), the last
+// stage scales by n^-1 with a mulmod.  Canonical outputs are the same for every schedule.
 template <int LOGN>
 __device__ __forceinline__ void ring_mul_row(double (&x)[4], const double (&sv)[4], int j, const ArithF64& ar,
                                              const double* __restrict__ tw, const double* __restrict__ itw,
@@ -60,7 +65,7 @@ __device__ __forceinline__ void ring_mul_row(double (&x)[4], const double (&sv)[
                 x[a] += mv;
             }
         }
-        if ((st & 1) || st == LOGN - 1)
+        if (st == 3)
 #pragma unroll
             for (int s = 0; s < 4; ++s) x[s] = ar.reduce(x[s]);
     }
@@ -69,8 +74,8 @@ __device__ __forceinline__ void ring_mul_row(double (&x)[4], const double (&sv)[
 #pragma unroll
     for (int st = LOGN - 1; st >= 0; --st) {   // inverse GS: X = u + v, Y = (u - v) W; m = 1 scales by n^-1
         const int m = 1 << st, lt = LOGN - 1 - st, t = 1 << lt;
-        const bool last = st == 0;
-        auto xsum = [&](double u) { return last ? ar.mulmod(u, ninv) : ar.reduce(u); };
+        const bool last = st == 0, lazy = (LOGN - 1 - st) % 2 == 0;
+        auto xsum = [&](double u) { return last ? ar.mulmod(u, ninv) : (lazy ? u : ar.reduce(u)); };
         if (t >= 4) {
             const int d = t >> 2;
             const bool up = j & d;
@@ -125,9 +130,9 @@ __device__ __forceinline__ void ring_mul_row64_lds(double (&x)[4], const double 
         x[i1] = x[i0] - mv;
         x[i0] += mv;
     };
-    auto gs = [&](int i0, int i1, double w, bool last) {
+    auto gs = [&](int i0, int i1, double w, bool last, bool lazy = false) {
         const double u = x[i0], v = x[i1];
-        x[i0] = last ? ar.mulmod(u + v, ninv) : ar.reduce(u + v);
+        x[i0] = last ? ar.mulmod(u + v, ninv) : (lazy ? u + v : ar.reduce(u + v));
         x[i1] = ar.mulmod(u - v, w);
     };
     auto red = [&]() {
@@ -149,7 +154,6 @@ __device__ __forceinline__ void ring_mul_row64_lds(double (&x)[4], const double 
     ct(1, 3, tw[1]);
     ct(0, 1, tw[2]);
     ct(2, 3, tw[3]);
-    red();
     xchg(sA, 16, sB, 4);
     ct(0, 2, tw[4 + b]);
     ct(1, 3, tw[4 + b]);
@@ -161,22 +165,21 @@ __device__ __forceinline__ void ring_mul_row64_lds(double (&x)[4], const double 
     ct(1, 3, tw[16 + j]);
     ct(0, 1, tw[32 + 2 * j]);
     ct(2, 3, tw[33 + 2 * j]);
-    red();
 #pragma unroll
     for (int m = 0; m < 4; ++m) x[m] = ar.mulmod(x[m], sv[m]);
     // inverse (GS, W = itw[m + e / 2t]; the last stage scales X by n^-1)
-    gs(0, 1, itw[32 + 2 * j], false);
-    gs(2, 3, itw[33 + 2 * j], false);
+    gs(0, 1, itw[32 + 2 * j], false, true);
+    gs(2, 3, itw[33 + 2 * j], false, true);
     gs(0, 2, itw[16 + j], false);
     gs(1, 3, itw[16 + j], false);
     xchg(sC, 1, sB, 4);
-    gs(0, 1, itw[8 + 2 * b], false);
-    gs(2, 3, itw[9 + 2 * b], false);
+    gs(0, 1, itw[8 + 2 * b], false, true);
+    gs(2, 3, itw[9 + 2 * b], false, true);
     gs(0, 2, itw[4 + b], false);
     gs(1, 3, itw[4 + b], false);
     xchg(sB, 4, sA, 16);
-    gs(0, 1, itw[2], false);
-    gs(2, 3, itw[3], false);
+    gs(0, 1, itw[2], false, true);
+    gs(2, 3, itw[3], false, true);
     gs(0, 2, itw[1], true);
     gs(1, 3, itw[1], true);
 }
