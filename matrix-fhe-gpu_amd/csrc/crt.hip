@@ -269,12 +269,16 @@ __device__ __forceinline__ bool compose_fast_f64(const uint64_t* __restrict__ in
     return ok;
 }
 
-// Limbs loaded per round of the fast path: every limb of a context with L <= MFHE_CRT_FAST_CH is loaded at once and
-// its residue check reads the registers (the reference's L = 11: one memory round trip instead of three -- 8 + 3
-// loads, then the check's re-reads)
+// Limbs loaded per round of the fast path: every limb of a context with L <= CH is loaded at once and its residue
+// check reads the registers (the reference's L = 11: one memory round trip instead of three -- 8 + 3 loads, then the
+// check's re-reads).  CH = 16 below 11 words; 32 from 11 words up (Q of >= 641 bits: the 32 x 50-bit primes of
+// BASELINE C5), where 16 made the check re-read all 32 residues -- with the nontemporal first reads, from HBM: twice
+// the compose's bytes (r06).
 #ifndef MFHE_CRT_FAST_CH
 #define MFHE_CRT_FAST_CH 16
 #endif
+template <int W>
+constexpr int crt_fast_ch() { return W >= 11 ? 32 : MFHE_CRT_FAST_CH; }
 
 // Small-value fast path.  With u = nearest integer to sum_k t_k/q_k, the centred CRT value is
 // X = sum_k t_k M_k - u Q; its low 64 bits cost one wrapping multiply-add per limb.  The candidate
@@ -291,7 +295,7 @@ __device__ __forceinline__ void compose_one(const uint64_t* __restrict__ in, uin
                                             const CrtLimbF* __restrict__ lf, bool qbig) {
     if (lf) {
         uint64_t a0;
-        if (compose_fast_f64<MFHE_CRT_FAST_CH>(in, ncoeff, L, Lg, shard_stride, lf, Q[0], Qh[0], qbig, a0, neg)) {
+        if (compose_fast_f64<crt_fast_ch<W>()>(in, ncoeff, L, Lg, shard_stride, lf, Q[0], Qh[0], qbig, a0, neg)) {
             mag[0] = a0;
 #pragma unroll
             for (int i = 1; i < W; ++i) mag[i] = 0;
