@@ -689,7 +689,7 @@ extern "C" int mfhe_ctx_set_option(mfhe_ctx* c, int opt, int64_t v) {
             c->wcrt_pipe = (int)v;
             return MFHE_OK;
         case MFHE_OPT_CGEMM_MFMA:
-            if (v < 0 || v > 2) return set_error(MFHE_EINVAL, "cgemm mfma must be 0, 1 or 2");
+            if (v < 0 || v > 3) return set_error(MFHE_EINVAL, "cgemm mfma must be 0 .. 3");
             c->cgemm_mfma = (int)v;
             return MFHE_OK;
         case MFHE_OPT_HE_FUSED:

@@ -1916,6 +1916,112 @@ int launch_mod_gemm(const ModGemmArgs& a, int L, hipStream_t s) {
     return MFHE_OK;
 }
 
+// ---- the per-lane XY product out = A M B in one launch (r06, n = 64) ----
+// he.hip xy3 at n = 64: A and B the shared 64 x 64 encoder matrices, M one lane's 64 x 64 block; one workgroup per
+// lane, eight waves of 16 x 32 outputs.  Phase 1 is cgemm_mfma_kernel<0>'s T = A M (v_mfma_f64_16x16x4_f64 blocks,
+// each output accumulated in the same order, k-step by k-step: first the Ar Br / Ar Bi terms, then -Ai Bi / Ai Br),
+// with all of K in LDS at once; T then goes to LDS instead of HBM and phase 2 is out = T B the same way.  So the
+// doubles are those of the two launches, without T's round trip and the second launch's fill.  LDS: A / T planes
+// [64][65] (the row pitch spreads a fragment's 16 rows over the banks), M / B planes [64][64]: 130.5 KiB, one
+// workgroup per CU, two waves per SIMD (four waves: 61.8 us per call; eight: 51.3 us; the two launches ~54 us).
+constexpr int XYN = 64, XYP = 65, XYT = 512;   // eight waves: two per SIMD at one workgroup per CU
+__global__ __launch_bounds__(XYT, 1) void xy_fused_kernel(const double2* __restrict__ A, const double2* __restrict__ M,
+                                                          const double2* __restrict__ Bm, double2* __restrict__ out) {
+    __shared__ double Lr[XYN * XYP], Li[XYN * XYP];   // left operand: A, then T   ([row][k])
+    __shared__ double Rr[XYN * XYN], Ri[XYN * XYN];   // right operand: M, then B  ([k][col])
+    const int t = threadIdx.x, lane = t & 63, w = t >> 6;
+    const int wm = (w >> 1) * 16, wp = (w & 1) * 32, r = lane & 15, kq = lane >> 4;   // each wave 16 x 32
+    const uint64_t lb = (uint64_t)blockIdx.x * XYN * XYN;
+    auto load_left = [&](const double2* src) {
+#pragma unroll 4
+        for (int e = 0; e < XYN * XYN / XYT; ++e) {
+            const int idx = t + e * XYT;
+            const double2 v = src[idx];
+            Lr[(idx >> 6) * XYP + (idx & 63)] = v.x;
+            Li[(idx >> 6) * XYP + (idx & 63)] = v.y;
+        }
+    };
+    auto load_right = [&](const double2* src) {
+#pragma unroll 4
+        for (int e = 0; e < XYN * XYN / XYT; ++e) {
+            const int idx = t + e * XYT;
+            const double2 v = src[idx];
+            Rr[idx] = v.x;
+            Ri[idx] = v.y;
+        }
+    };
+    v4d cr[1][2], ci[1][2];
+    auto product = [&]() {
+#pragma unroll
+        for (int i = 0; i < 1; ++i)
+#pragma unroll
+            for (int j = 0; j < 2; ++j) cr[i][j] = ci[i][j] = v4d{0, 0, 0, 0};
+#pragma unroll 4
+        for (int ks = 0; ks < XYN / 4; ++ks) {
+            const int k = ks * 4 + kq;
+            double ar[1], ai[1], nai[1], br[2], bi[2];
+#pragma unroll
+            for (int i = 0; i < 1; ++i) {
+                ar[i] = Lr[(wm + 16 * i + r) * XYP + k];
+                ai[i] = Li[(wm + 16 * i + r) * XYP + k];
+                nai[i] = -ai[i];
+            }
+#pragma unroll
+            for (int j = 0; j < 2; ++j) {
+                br[j] = Rr[k * XYN + wp + 16 * j + r];
+                bi[j] = Ri[k * XYN + wp + 16 * j + r];
+            }
+#pragma unroll
+            for (int i = 0; i < 1; ++i)
+#pragma unroll
+                for (int j = 0; j < 2; ++j) {
+                    cr[i][j] = __builtin_amdgcn_mfma_f64_16x16x4f64(ar[i], br[j], cr[i][j], 0, 0, 0);
+                    ci[i][j] = __builtin_amdgcn_mfma_f64_16x16x4f64(ar[i], bi[j], ci[i][j], 0, 0, 0);
+                }
+#pragma unroll
+            for (int i = 0; i < 1; ++i)
+#pragma unroll
+                for (int j = 0; j < 2; ++j) {
+                    cr[i][j] = __builtin_amdgcn_mfma_f64_16x16x4f64(nai[i], bi[j], cr[i][j], 0, 0, 0);
+                    ci[i][j] = __builtin_amdgcn_mfma_f64_16x16x4f64(ai[i], br[j], ci[i][j], 0, 0, 0);
+                }
+        }
+    };
+    load_left(A);
+    load_right(M + lb);
+    __syncthreads();
+    product();   // T = A M
+    __syncthreads();   // every wave is done reading A and M
+#pragma unroll
+    for (int i = 0; i < 1; ++i)
+#pragma unroll
+        for (int j = 0; j < 2; ++j)
+#pragma unroll
+            for (int g = 0; g < 4; ++g) {
+                const int m = wm + 16 * i + kq + 4 * g, p = wp + 16 * j + r;
+                Lr[m * XYP + p] = cr[i][j][g];
+                Li[m * XYP + p] = ci[i][j][g];
+            }
+    load_right(Bm);
+    __syncthreads();
+    product();   // out = T B
+    double2* o = out + lb;
+#pragma unroll
+    for (int i = 0; i < 1; ++i)
+#pragma unroll
+        for (int j = 0; j < 2; ++j)
+#pragma unroll
+            for (int g = 0; g < 4; ++g)
+                o[(wm + 16 * i + kq + 4 * g) * XYN + wp + 16 * j + r] = make_double2(cr[i][j][g], ci[i][j][g]);
+}
+
+int launch_xy_fused(const double2* A, const double2* M, const double2* B, double2* out, int lanes, hipStream_t s) {
+    if (!A || !M || !B || !out || lanes <= 0) return set_error(MFHE_EINVAL, "xy_fused: bad arguments");
+    hipLaunchKernelGGL(xy_fused_kernel, dim3((uint32_t)lanes), dim3(XYT), 0, s, A, M, B, out);
+    MFHE_CHECK_LAUNCH("xy_fused_kernel");
+    return MFHE_OK;
+}
+
 int launch_cgemm(const CGemmArgs& a, int batch, hipStream_t s) {
     dim3 grid((a.P + TP - 1) / TP, (a.M + TM - 1) / TM, batch);
     if (a.mfma) {

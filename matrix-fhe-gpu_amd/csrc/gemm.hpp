@@ -107,6 +107,9 @@ int launch_mod_gemm_smallb(const ModGemmArgs& a, const int8_t* b8, int L, hipStr
 // two independent W-CRT transforms of the same shape as one launch per step (gemm.hip; he.hip encode / decode)
 int launch_mod_gemm_pair(const ModGemmArgs& a, const ModGemmArgs& b, int L, hipStream_t s);
 int launch_cgemm(const CGemmArgs& a, int batch, hipStream_t s);
+// out = A M B per lane for 64 x 64 complex blocks (A, B shared; M, out [lanes][64][64]) in one launch: the two
+// launch_cgemm products of he.hip xy3 without the intermediate's HBM round trip, the same doubles (gemm.hip)
+int launch_xy_fused(const double2* A, const double2* M, const double2* B, double2* out, int lanes, hipStream_t s);
 // factored inverse W-DFT, first step: per column the rows r2 = 0, 255, 256 of E_a by dot products (xpow [2][256]:
 // zeta^(-255 b), zeta^(-256 b)), then f_0, f_257 into out and (c0, c1) into a.cc (gemm.hip)
 int launch_cwdft_inv_dots(const CGemmArgs& a, const double2* in, const double2* xpow, hipStream_t s);

@@ -634,7 +634,7 @@ static int wcrt_gemm(mfhe_ctx* c, const uint64_t* A, const uint64_t* B, bool b_p
 // (gemm.hip cgemm_mfma_kernel<1 / 2>), half the flops of the dense 512 x 512 product
 static int wdft(mfhe_ctx* c, const double2* A, const double2* in, double2* out, hipStream_t s) {
     const Geo2 g = geo(c);
-    if (c->cgemm_mfma == 2 && c->d_wdZ && (A == c->d_wdV || A == c->d_wdVinv)) {
+    if (c->cgemm_mfma >= 2 && c->d_wdZ && (A == c->d_wdV || A == c->d_wdVinv)) {
         CGemmArgs f;
         f.mfma = true;
         f.B = in;
@@ -680,6 +680,9 @@ static int wdft(mfhe_ctx* c, const double2* A, const double2* in, double2* out, 
 static int xy3(const mfhe_ctx* c, const double2* A, const double2* in, const double2* B, double2* tmp, double2* out,
                size_t lanes, hipStream_t s) {
     const Geo2 g = geo(c);
+    // n = 64 with the MFMA path: both products in one launch (gemm.hip xy_fused_kernel; MFHE_OPT_CGEMM_MFMA 3 keeps
+    // the two launches), the same doubles
+    if (c->cgemm_mfma == 2 && g.n == 64 && in != out) return launch_xy_fused(A, in, B, out, (int)lanes, s);
     CGemmArgs a;
     a.mfma = c->cgemm_mfma != 0;
     a.M = a.K = (int)g.n;

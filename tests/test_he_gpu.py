@@ -110,10 +110,10 @@ def test_wcrt_centered_matches_reference_semantics(mfhe, orc, small):
     np.testing.assert_array_equal(rt1.cpu().numpy(), coeff)
 
 
-@pytest.mark.parametrize("cgemm", [2, 1, 0])
+@pytest.mark.parametrize("cgemm", [2, 3, 1, 0])
 def test_wdft_and_xy_transforms_vs_oracle(mfhe, orc, small, cgemm):
     """W-DFT / XY transforms on the f64 MFMA complex GEMM with the W-DFT factored through 771 = 3 x 257 (2,
-    default), dense (1), and the VALU kernel (0)."""
+    default; 3: the XY products as two launches), dense (1), and the VALU kernel (0)."""
     n, ctx, h = small
     prev = ctx.get_option(mfhe.OPT_CGEMM_MFMA)
     ctx.set_option(mfhe.OPT_CGEMM_MFMA, cgemm)
@@ -128,7 +128,9 @@ def test_cgemm_mfma_matches_valu(mfhe, n):
     """f64 MFMA complex GEMM (gemm.hip cgemm_mfma_kernel) vs the VALU kernel at tile-ragged and full sizes:
     XY-IDFT / XY-DFT (M = K = P = n per lane) and W-DFT / W-IDFT (M = K = 512, P = n^2), 1e-12 relative; the
     factored W-DFT (mode 2, default) too: its 256 x 256 zeta tables are single cos / sin values while the dense V
-    (HE.cu:282-290) is a chain of products, so the two agree to rounding, not bit for bit."""
+    (HE.cu:282-290) is a chain of products, so the two agree to rounding, not bit for bit.  At n = 64 mode 2 runs
+    both XY products of a lane in one launch (gemm.hip xy_fused_kernel, r06): the same doubles as the two launches
+    of modes 3 and 1, bit for bit."""
     import torch
     ctx = mfhe.Context(RNS[:2], n.bit_length() - 1, CONV)
     assert ctx.get_option(mfhe.OPT_CGEMM_MFMA) == 2
@@ -137,7 +139,7 @@ def test_cgemm_mfma_matches_valu(mfhe, n):
     z = (rng.standard_normal(512 * n2) + 1j * rng.standard_normal(512 * n2)).astype(np.complex128)
     zt = torch.from_numpy(z.view(np.float64).copy()).cuda()
     outs = {}
-    for mode in (2, 1, 0):
+    for mode in (2, 3, 1, 0):
         ctx.set_option(mfhe.OPT_CGEMM_MFMA, mode)
         assert ctx.get_option(mfhe.OPT_CGEMM_MFMA) == mode
         res = []
@@ -151,9 +153,16 @@ def test_cgemm_mfma_matches_valu(mfhe, n):
             res.append(o)
         torch.cuda.synchronize()
         outs[mode] = [r.cpu().numpy() for r in res]
-    for mode in (2, 1):
+    for mode in (2, 3, 1):
         for a, b in zip(outs[mode], outs[0]):
             assert np.max(np.abs(a - b)) <= 1e-12 * np.max(np.abs(b)), mode
+    for i in range(2):   # XY: one launch (2) == two launches (3, 1)
+        np.testing.assert_array_equal(outs[2][i], outs[3][i])
+        np.testing.assert_array_equal(outs[2][i], outs[1][i])
+    for i in range(2, 4):   # the factored W-DFT of modes 2 and 3
+        np.testing.assert_array_equal(outs[2][i], outs[3][i])
+    with pytest.raises(mfhe.MfheError):
+        ctx.set_option(mfhe.OPT_CGEMM_MFMA, 4)
 
 
 def _wdft_and_xy_transforms(mfhe, orc, n, ctx):
