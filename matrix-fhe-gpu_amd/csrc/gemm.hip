@@ -626,16 +626,31 @@ __global__ __launch_bounds__(256, 4) void mfma_digitize_fold_kernel(const uint64
 #pragma unroll
             for (int c = 0; c < 4; ++c) pk[ap][i][c] = 0;
     const int rb = kc * 32 + hf * 16 + 1;
-    int r1 = rb % 3;
+    // r06: F_a = omega^(a r1) (x1 + omega^(2a) x2) and omega^2 = -1 - omega, so with m = omega x2
+    //   F_1 = omega^r1 (x1 - x2 - m),  F_2 = omega^(2 r1) (x1 + m)
+    // -- three modmuls per r2 instead of four (|x1 - x2 - m| <= 3q: inside mulmod's |v| <= 4q); the same residues,
+    // other representatives, so other digits but the same GEMM result mod q.  The weights omega^(a r1) are rotated
+    // once to this thread's first r2 mod 3, so the unrolled loop indexes them by kk % 3 (the per-row selects by a
+    // runtime r1 were ~200 of the kernel's ~1830 VALU instructions).
+    const double omega = c1[0][1];
+    const int r10 = rb % 3;
+    double wr[2][3];
+#pragma unroll
+    for (int ap = 0; ap < 2; ++ap)
+#pragma unroll
+        for (int j = 0; j < 3; ++j) {
+            const int e0 = j, e1 = (j + 1) % 3, e2 = (j + 2) % 3;   // (r10 + j) mod 3 for r10 = 0, 1, 2
+            wr[ap][j] = r10 == 0 ? c1[ap][e0] : (r10 == 1 ? c1[ap][e1] : c1[ap][e2]);
+        }
 #pragma unroll
     for (int kk = 0; kk < 16; ++kk) {
         const int r2 = rb + kk;
         const double x1 = in(r2), x2r = in(r2 + 257 < 512 ? r2 + 257 : 511), x2 = r2 + 257 < 512 ? x2r : 0.0;
+        const double m = ar.mulmod(x2, omega);
+        const double fin[2] = {x1 - x2 - m, x1 + m};
 #pragma unroll
         for (int ap = 0; ap < 2; ++ap) {
-            const double w1 = r1 == 0 ? c1[ap][0] : (r1 == 1 ? c1[ap][1] : c1[ap][2]);
-            const double w2 = r1 == 0 ? c2[ap][0] : (r1 == 1 ? c2[ap][1] : c2[ap][2]);
-            const double v = ar.reduce(ar.mulmod(x1, w1) + ar.mulmod(x2, w2));   // |v| <= q/2 + eps
+            const double v = ar.reduce(ar.mulmod(fin[ap], wr[ap][kk % 3]));   // |v| <= q/2 + eps
             const uint64_t y = balanced_bytes<D>(v);
             const uint32_t lo = (uint32_t)y, hi = (uint32_t)(y >> 32);
 #pragma unroll
@@ -644,7 +659,6 @@ __global__ __launch_bounds__(256, 4) void mfma_digitize_fold_kernel(const uint64
                 pk[ap][i][kk >> 2] |= b << (8 * (kk & 3));
             }
         }
-        r1 = r1 == 2 ? 0 : r1 + 1;
     }
     if (kc == 0 && hf == 0) {
         const double x1 = in(0), x2 = in(257);
