@@ -198,6 +198,16 @@ __device__ __forceinline__ double dpp_swap1(double x) {
                             __builtin_amdgcn_mov_dpp(lo, 0xB1, 0xF, 0xF, true));
 }
 
+// one output of the factored inverse W-DFT: interleaved complex, or planar (CGemmArgs::Cim)
+__device__ __forceinline__ void cstore(const CGemmArgs& a, uint64_t idx, double re, double im) {
+    if (a.Cim) {
+        ((double*)a.C)[idx] = re;
+        a.Cim[idx] = im;
+    } else {
+        a.C[idx] = make_double2(re, im);
+    }
+}
+
 // FAC (a.fac): 0 dense; 1 / 2 the factored forward / inverse W-DFT (gemm.hpp CGemmArgs::fac)
 template <int FAC>
 __global__ __launch_bounds__(NTH, 2) void cgemm_mfma_kernel(CGemmArgs a) {
@@ -347,7 +357,7 @@ __global__ __launch_bounds__(NTH, 2) void cgemm_mfma_kernel(CGemmArgs a) {
                     const int jr = ap ? r2 + 257 : r2;
                     if (live && jr < 512) {
                         const double f0 = (double)a.phi[jr], f1 = (double)a.phi[jr - 1];
-                        C[(uint64_t)jr * a.scM + p] = make_double2(hx - c0.x * f0 - c1.x * f1, hy - c0.y * f0 - c1.y * f1);
+                        cstore(a, (uint64_t)jr * a.scM + p, hx - c0.x * f0 - c1.x * f1, hy - c0.y * f0 - c1.y * f1);
                     }
                 }
         }
@@ -421,11 +431,11 @@ __global__ __launch_bounds__(256) void cwdft_inv_dots_kernel(CGemmArgs a, const 
     const double2 c0 = make_double2(h512.x - c1.x * p511, h512.y - c1.y * p511);
     if (!live) return;
     if (ap == 0) {
-        a.C[p] = make_double2(h0.x - c0.x * p0, h0.y - c0.y * p0);
+        cstore(a, p, h0.x - c0.x * p0, h0.y - c0.y * p0);
         ((double2*)a.cc)[2ull * p] = c0;
         ((double2*)a.cc)[2ull * p + 1] = c1;
     } else {
-        a.C[257ull * a.scM + p] = make_double2(h257.x - c0.x * p257 - c1.x * p256, h257.y - c0.y * p257 - c1.y * p256);
+        cstore(a, 257ull * a.scM + p, h257.x - c0.x * p257 - c1.x * p256, h257.y - c0.y * p257 - c1.y * p256);
     }
 }
 
@@ -619,12 +629,7 @@ __global__ __launch_bounds__(256, 4) void mfma_digitize_fold_kernel(const uint64
         return live ? x : 0.0;
     };
     uint32_t pk[2][D][4];
-#pragma unroll
-    for (int ap = 0; ap < 2; ++ap)
-#pragma unroll
-        for (int i = 0; i < D; ++i)
-#pragma unroll
-            for (int c = 0; c < 4; ++c) pk[ap][i][c] = 0;
+    uint32_t ylo[2][4], yhi[2][4];   // the current group of four rows' digit words
     const int rb = kc * 32 + hf * 16 + 1;
     // r06: F_a = omega^(a r1) (x1 + omega^(2a) x2) and omega^2 = -1 - omega, so with m = omega x2
     //   F_1 = omega^r1 (x1 - x2 - m),  F_2 = omega^(2 r1) (x1 + m)
@@ -652,12 +657,25 @@ __global__ __launch_bounds__(256, 4) void mfma_digitize_fold_kernel(const uint64
         for (int ap = 0; ap < 2; ++ap) {
             const double v = ar.reduce(ar.mulmod(fin[ap], wr[ap][kk % 3]));   // |v| <= q/2 + eps
             const uint64_t y = balanced_bytes<D>(v);
-            const uint32_t lo = (uint32_t)y, hi = (uint32_t)(y >> 32);
+            ylo[ap][kk & 3] = (uint32_t)y;
+            yhi[ap][kk & 3] = (uint32_t)(y >> 32);
+        }
+        if ((kk & 3) == 3) {
+            // byte transpose of four rows' digits into the planes' words: plane i's word = byte i of rows 0..3.
+            // v_perm_b32 picks 4 of the 8 bytes of (S0:S1): first rows (0, 1) and (2, 3) interleaved for two planes
+            // at once, then the two halves joined -- 3 perms per two planes instead of a shift, mask and or per byte
 #pragma unroll
-            for (int i = 0; i < D; ++i) {
-                const uint32_t b = i < 4 ? (lo >> (8 * i)) & 255u : (hi >> (8 * (i - 4))) & 255u;
-                pk[ap][i][kk >> 2] |= b << (8 * (kk & 3));
-            }
+            for (int ap = 0; ap < 2; ++ap)
+#pragma unroll
+                for (int pi = 0; pi < D; pi += 2) {
+                    const uint32_t* src = pi < 4 ? ylo[ap] : yhi[ap];
+                    const uint32_t i = (uint32_t)(pi & 3), j = i + 1;
+                    const uint32_t sel = i | ((4 + i) << 8) | (j << 16) | ((4 + j) << 24);
+                    const uint32_t t01 = __builtin_amdgcn_perm(src[1], src[0], sel);
+                    const uint32_t t23 = __builtin_amdgcn_perm(src[3], src[2], sel);
+                    pk[ap][pi][kk >> 2] = __builtin_amdgcn_perm(t23, t01, 0x05040100u);
+                    if (pi + 1 < D) pk[ap][pi + 1][kk >> 2] = __builtin_amdgcn_perm(t23, t01, 0x07060302u);
+                }
         }
     }
     if (kc == 0 && hf == 0) {

@@ -98,6 +98,9 @@ struct CGemmArgs {
     const double2* cc = nullptr;    // fac 2: [Pf][2] (c0, c1)
     const double2* lam = nullptr;   // fac 2: [2: lam1, lam2][2: a'][3: t]
     const int8_t* phi = nullptr;    // fac 2: [513] Phi_771 coefficients
+    double* Cim = nullptr;          // fac 2 only: planar output -- the real parts at (double*)C, the imaginary at Cim,
+                                    // element (row, p) at row * scM + p in each (he.hip encode: the fold then reads
+                                    // 8-byte lanes, not every other double of 16-byte pairs)
 };
 
 int launch_mod_gemm(const ModGemmArgs& a, int L, hipStream_t s);

@@ -632,8 +632,12 @@ static int wcrt_gemm(mfhe_ctx* c, const uint64_t* A, const uint64_t* B, bool b_p
 
 // complex W-DFT / W-IDFT over [phi][n2]; MFHE_OPT_CGEMM_MFMA = 2 (default): factored through 771 = 3 x 257
 // (gemm.hip cgemm_mfma_kernel<1 / 2>), half the flops of the dense 512 x 512 product
-static int wdft(mfhe_ctx* c, const double2* A, const double2* in, double2* out, hipStream_t s) {
+// planar (factored W-IDFT only, wdft_planar_ok): out as two [phi][n2] double planes, real then imaginary
+static bool wdft_planar_ok(const mfhe_ctx* c) { return c->cgemm_mfma >= 2 && c->d_wdZ; }
+static int wdft(mfhe_ctx* c, const double2* A, const double2* in, double2* out, hipStream_t s, bool planar = false) {
     const Geo2 g = geo(c);
+    if (planar && !(wdft_planar_ok(c) && A == c->d_wdVinv))
+        return set_error(MFHE_EINVAL, "wdft: planar output needs the factored W-IDFT");
     if (c->cgemm_mfma >= 2 && c->d_wdZ && (A == c->d_wdV || A == c->d_wdVinv)) {
         CGemmArgs f;
         f.mfma = true;
@@ -658,6 +662,7 @@ static int wdft(mfhe_ctx* c, const double2* A, const double2* in, double2* out, 
             c->wd_ws_bytes = need;
         }
         f.fac = 2;
+        if (planar) f.Cim = (double*)out + 512ull * g.n2;
         f.A = c->d_wdZi;
         f.cc = (const double2*)c->wd_ws;
         f.lam = c->d_wdlam;
@@ -754,23 +759,28 @@ static int encode_impl(mfhe_ctx* c, const double* msg, uint64_t* out_re, uint64_
     uint64_t* cre = b.get<uint64_t>(g.words);
     // 1) XY-IDFT per lane (Encoder::idft2, encoder.cu:460-467)
     RC(xy3(c, c->d_encVi, (const double2*)msg, c->d_encViT, tmp, xy, 512, s));
-    // 2) W-IDFT (w_idft_kernel, batched_encoder.cu:104-123)
-    RC(wdft(c, c->d_wdVinv, xy, tmp, s));
+    // 2) W-IDFT (w_idft_kernel, batched_encoder.cu:104-123); planar (real plane, then imaginary) when the fused
+    // digitize reads it, so each of its per-limb passes reads whole 8-byte lanes (r06)
+    const bool planar = quant_fused_ok(c) && wdft_planar_ok(c);
+    RC(wdft(c, c->d_wdVinv, xy, tmp, s, planar));
     // 3) quantize + RNS split, 4) W-CRT -> matrix-major eval (re, then im); fused into the W-CRT's digitize
     // kernel when the factored forward runs (the residues never reach HBM)
     if (quant_fused_ok(c)) {
+        const double* qre = (const double*)tmp;
+        const double* qim = planar ? qre + 512ull * g.n2 : qre + 1;
+        const uint64_t qstep = planar ? 1 : 2;
         if (c->he_streams >= 2) {   // modes 2, 3: re and im as one launch per step (gemm.hip launch_mod_gemm_pair)
             ModGemmArgs ar, ai;
-            RC(wcrt_args(c, ar, c->d_wV, (const uint64_t*)tmp, false, out_re, WOut::Matrix, false, 1, (const double*)tmp, 2));
-            RC(wcrt_args(c, ai, c->d_wV, (const uint64_t*)tmp, false, out_im, WOut::Matrix, false, 1, (const double*)tmp + 1,
-                         2, nullptr, 1));
+            RC(wcrt_args(c, ar, c->d_wV, (const uint64_t*)tmp, false, out_re, WOut::Matrix, false, 1, qre, qstep));
+            RC(wcrt_args(c, ai, c->d_wV, (const uint64_t*)tmp, false, out_im, WOut::Matrix, false, 1, qim, qstep,
+                         nullptr, 1));
             return launch_mod_gemm_pair(ar, ai, g.L, s);
         }
         HeFork f;
         RC(f.begin(c, s, c->he_streams == 1));
-        RC(wcrt_gemm(c, c->d_wV, (const uint64_t*)tmp, false, out_re, WOut::Matrix, false, s, 1, (const double*)tmp, 2));
-        RC(wcrt_gemm(c, c->d_wV, (const uint64_t*)tmp, false, out_im, WOut::Matrix, false, f.x, 1, (const double*)tmp + 1,
-                     2, nullptr, f.on ? 1 : 0));
+        RC(wcrt_gemm(c, c->d_wV, (const uint64_t*)tmp, false, out_re, WOut::Matrix, false, s, 1, qre, qstep));
+        RC(wcrt_gemm(c, c->d_wV, (const uint64_t*)tmp, false, out_im, WOut::Matrix, false, f.x, 1, qim, qstep,
+                     nullptr, f.on ? 1 : 0));
         return f.join();
     }
     RC(mfhe_rns_decompose(c, (const double*)tmp, 2, 512, g.n2, cre, (mfhe_stream_t)s));
