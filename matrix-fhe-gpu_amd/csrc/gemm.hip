@@ -472,6 +472,26 @@ __device__ __forceinline__ uint64_t balanced_bytes(double v) {   // v integral, 
     constexpr uint64_t kOff = 0x8080808080808080ull >> (64 - 8 * D);
     return (uint64_t)__double_as_longlong(v + kMagic) - ((uint64_t)__double_as_longlong(kMagic) - kOff);
 }
+// Byte transpose of digit words into digit-plane words (r06): rows 4c .. 4c + 3 of y (each row's D digit bytes in
+// its low D bytes) give word c of every plane i = byte i of those four rows.  v_perm_b32 picks 4 of the 8 bytes of
+// (S0:S1): rows (0, 1) and (2, 3) interleaved for two planes at once, then the halves joined -- three perms per two
+// planes and four rows, instead of a shift, mask and or per byte.
+template <int D, int R>
+__device__ __forceinline__ void pack_planes(const uint64_t (&y)[R], uint32_t (&pk)[D][R / 4]) {
+#pragma unroll
+    for (int c = 0; c < R / 4; ++c)
+#pragma unroll
+        for (int pi = 0; pi < D; pi += 2) {
+            const int sh = pi < 4 ? 0 : 32;
+            const uint32_t i = (uint32_t)(pi & 3), j = i + 1;
+            const uint32_t sel = i | ((4 + i) << 8) | (j << 16) | ((4 + j) << 24);
+            const uint32_t t01 = __builtin_amdgcn_perm((uint32_t)(y[4 * c + 1] >> sh), (uint32_t)(y[4 * c] >> sh), sel);
+            const uint32_t t23 = __builtin_amdgcn_perm((uint32_t)(y[4 * c + 3] >> sh), (uint32_t)(y[4 * c + 2] >> sh), sel);
+            pk[pi][c] = __builtin_amdgcn_perm(t23, t01, 0x05040100u);
+            if (pi + 1 < D) pk[pi + 1][c] = __builtin_amdgcn_perm(t23, t01, 0x07060302u);
+        }
+}
+
 // digit planes the GEMM reads per limb (max(limbD, 5), <= D): planes past it are never read, so never written
 struct PlaneCounts {
     uint8_t n[64];   // limbs >= 64: all D
@@ -493,22 +513,22 @@ __global__ __launch_bounds__(256) void mfma_digitize_kernel(const uint64_t* __re
     if (p >= Ppad) return;
     const uint64_t* Bl = B + (uint64_t)l * bL;
     const uint64_t col = (uint64_t)(p >> log_n) * sbY + (p & ((1u << log_n) - 1));
-    uint32_t pk[D][8];   // plane i, bytes 4c..4c+3 of the panel's 32 k (byte v is the digit mod 256)
+    // plane i, bytes 4c..4c+3 of the panel's 32 k.  Balanced digits by the offset rule: the bytes of x + 0x80..80
+    // (D bytes; x < 2^(8D - 1)) are the digits + 128, so byte ^ 0x80 is the digit mod 256 (r05: a shift-and-carry
+    // loop per digit; the same bytes)
+    constexpr uint64_t kOff = 0x8080808080808080ull >> (64 - 8 * D);
+    uint64_t y[32];
+#pragma unroll
+    for (int kk = 0; kk < 32; ++kk) {
+        const uint64_t x = Bl[(uint64_t)(kc * 32 + kk) * sbK + (p < P ? col : 0)];
+        y[kk] = (p < P ? x : 0) + kOff;
+    }
+    uint32_t pk[D][8];
+    pack_planes<D, 32>(y, pk);
 #pragma unroll
     for (int i = 0; i < D; ++i)
 #pragma unroll
-        for (int c = 0; c < 8; ++c) pk[i][c] = 0;
-#pragma unroll
-    for (int kk = 0; kk < 32; ++kk) {
-        uint64_t x = Bl[(uint64_t)(kc * 32 + kk) * sbK + (p < P ? col : 0)];
-        x = p < P ? x : 0;
-#pragma unroll
-        for (int i = 0; i < D; ++i) {
-            const uint32_t v = (uint32_t)x & 255u;
-            x = (x >> 8) + (v >> 7);                 // balanced digits: v >= 128 stands for v - 256
-            pk[i][kk >> 2] |= v << (8 * (kk & 3));
-        }
-    }
+        for (int c = 0; c < 8; ++c) pk[i][c] ^= 0x80808080u;
     const int nd = l < 64 ? pc.n[l] : D;
 #pragma unroll
     for (int i = 0; i < D; ++i) {
@@ -737,10 +757,6 @@ __global__ __launch_bounds__(256) void mfma_digitize_ifold_kernel(ModGemmArgs a,
     for (int pn = 0; pn < 2; ++pn) {
         const int kc = 2 * kq + pn, k0 = kc * 32 + hf * 16;
         uint32_t pk[D][4];
-#pragma unroll
-        for (int i = 0; i < D; ++i)
-#pragma unroll
-            for (int c = 0; c < 4; ++c) pk[i][c] = 0;
         double v[16];
 #pragma unroll
         for (int kk = 0; kk < 16; ++kk)   // b = k0 + kk + 1
@@ -760,15 +776,11 @@ __global__ __launch_bounds__(256) void mfma_digitize_ifold_kernel(ModGemmArgs a,
         s0 = ar.reduce(s0 + t0);
         s1 = ar.reduce(s1 + ar.mulmod(h1, zp[(k0 >> 4)]));
         s2 = ar.reduce(s2 + ar.mulmod(h2, zp[16 + (k0 >> 4)]));
+        {
+            uint64_t y[16];
 #pragma unroll
-        for (int kk = 0; kk < 16; ++kk) {
-            const uint64_t y = balanced_bytes<D>(v[kk]);
-            const uint32_t lo = (uint32_t)y, hi = (uint32_t)(y >> 32);
-#pragma unroll
-            for (int i = 0; i < D; ++i) {
-                const uint32_t b = i < 4 ? (lo >> (8 * i)) & 255u : (hi >> (8 * (i - 4))) & 255u;
-                pk[i][kk >> 2] |= b << (8 * (kk & 3));
-            }
+            for (int kk = 0; kk < 16; ++kk) y[kk] = balanced_bytes<D>(v[kk]);
+            pack_planes<D, 16>(y, pk);
         }
 #pragma unroll
         for (int i = 0; i < D; ++i) {
@@ -962,19 +974,11 @@ __device__ __forceinline__ void ifold_dec_impl(const ModGemmArgs& a, uint32_t Pp
         s1 = ar.reduce(s1 + ar.mulmod(h1, zp[(k0 >> 4)]));
         s2 = ar.reduce(s2 + ar.mulmod(h2, zp[16 + (k0 >> 4)]));
         uint32_t pk[D][4];
+        {
+            uint64_t yb[16];
 #pragma unroll
-        for (int i = 0; i < D; ++i)
-#pragma unroll
-            for (int c = 0; c < 4; ++c) pk[i][c] = 0;
-#pragma unroll
-        for (int kk = 0; kk < 16; ++kk) {
-            const uint64_t yb = balanced_bytes<D>(v[kk]);
-            const uint32_t lo = (uint32_t)yb, hi = (uint32_t)(yb >> 32);
-#pragma unroll
-            for (int i = 0; i < D; ++i) {
-                const uint32_t b = i < 4 ? (lo >> (8 * i)) & 255u : (hi >> (8 * (i - 4))) & 255u;
-                pk[i][kk >> 2] |= b << (8 * (kk & 3));
-            }
+            for (int kk = 0; kk < 16; ++kk) yb[kk] = balanced_bytes<D>(v[kk]);
+            pack_planes<D, 16>(yb, pk);
         }
 #pragma unroll
         for (int i = 0; i < D; ++i) {
