@@ -629,18 +629,33 @@ __global__ __launch_bounds__(256, 4) void mfma_digitize_fold_kernel(const uint64
         uq = fs.qmu[2 * l];
         umu = fs.qmu[2 * l + 1];
     }
+    // SRC 2: the sampler's LCG output for row r, (123456789 + ((r Ltot + lbase + l) << 2 log n) + p) A + C mod 2^64
+    // (he.hip uniform_kernel).  It is affine in r: with the per-row step K = (Ltot << 2 log n) A, row r + 1's word is
+    // row r's + K, and row r + 257's is row r's + 257 K -- 64-bit adds in the row loop instead of a 64-bit multiply
+    // per value, the same words (sampled_row below; in(r) keeps the direct form for the d0 rows).
+    uint64_t lcgK = 0, lcgK257 = 0;
+    if constexpr (SRC == 2) {
+        lcgK = ((uint64_t)fs.Ltot << (2 * log_n)) * 6364136223846793005ULL;
+        lcgK257 = lcgK * 257ull;
+    }
+    auto lcg_seed = [&](int r) {
+        const uint32_t pp = live ? p : 0;
+        return (123456789ULL + (((uint64_t)r * (uint64_t)fs.Ltot + (uint64_t)(fs.lbase + l)) << (2 * log_n)) + pp) *
+                   6364136223846793005ULL + 1442695040888963407ULL;
+    };
+    auto sampled = [&](uint64_t seed) {   // Barrett as uniform_kernel: [0, 3q), then two selects
+        uint64_t v = seed - __umul64hi(seed, umu) * uq;
+        v = v >= uq ? v - uq : v;
+        v = v >= uq ? v - uq : v;
+        return live ? ArithF64::from_u64(v) : 0.0;
+    };
     auto in = [&](int r) {
         double x;
         const uint32_t pp = live ? p : 0;
         if constexpr (SRC == 1) {
             x = ar.reduce(round(qf[(uint64_t)r * qf_row + (uint64_t)pp * qf_step] * delta));
         } else if constexpr (SRC == 2) {
-            uint64_t seed = 123456789ULL + (((uint64_t)r * (uint64_t)fs.Ltot + (uint64_t)(fs.lbase + l)) << (2 * log_n)) + pp;
-            seed = seed * 6364136223846793005ULL + 1442695040888963407ULL;
-            uint64_t v = seed - __umul64hi(seed, umu) * uq;   // Barrett as uniform_kernel: [0, 3q)
-            v = v >= uq ? v - uq : v;
-            v = v >= uq ? v - uq : v;
-            x = ArithF64::from_u64(v);
+            return sampled(lcg_seed(r));
         } else if constexpr (SRC == 3) {
             x = qf[(uint64_t)r * qf_row + pp];
         } else {
@@ -667,10 +682,21 @@ __global__ __launch_bounds__(256, 4) void mfma_digitize_fold_kernel(const uint64
             const int e0 = j, e1 = (j + 1) % 3, e2 = (j + 2) % 3;   // (r10 + j) mod 3 for r10 = 0, 1, 2
             wr[ap][j] = r10 == 0 ? c1[ap][e0] : (r10 == 1 ? c1[ap][e1] : c1[ap][e2]);
         }
+    uint64_t seed1 = 0;
+    if constexpr (SRC == 2) seed1 = lcg_seed(rb);
 #pragma unroll
     for (int kk = 0; kk < 16; ++kk) {
         const int r2 = rb + kk;
-        const double x1 = in(r2), x2r = in(r2 + 257 < 512 ? r2 + 257 : 511), x2 = r2 + 257 < 512 ? x2r : 0.0;
+        double x1, x2r;
+        if constexpr (SRC == 2) {
+            x1 = sampled(seed1);
+            x2r = sampled(seed1 + lcgK257);   // row r2 + 257 (unused past row 511)
+            seed1 += lcgK;
+        } else {
+            x1 = in(r2);
+            x2r = in(r2 + 257 < 512 ? r2 + 257 : 511);
+        }
+        const double x2 = r2 + 257 < 512 ? x2r : 0.0;
         const double m = ar.mulmod(x2, omega);
         const double fin[2] = {x1 - x2 - m, x1 + m};
 #pragma unroll
