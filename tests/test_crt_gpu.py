@@ -183,10 +183,13 @@ def test_crt_compose_f64_sharded_matches_unsharded(mfhe, orc, world, small):
         assert torch.equal(got, ref)
 
 
-@pytest.mark.parametrize("L,W", [(1, None), (1, 7), (2, None), (8, None), (9, None), (11, 7), (16, None), (32, None)])
+@pytest.mark.parametrize("L,W", [(1, None), (1, 7), (2, None), (8, None), (9, None), (11, 7), (16, None), (24, None),
+                                 (32, None), (40, None)])
 def test_crt_compose_small_value_fast_path_boundaries(mfhe, orc, L, W):
     """Centred values around the fast path's limits (|X| near 2^62, near Q/2 for small Q) must match the
-    full multi-word compose bit-exactly (oracle), whichever path the kernel takes."""
+    full multi-word compose bit-exactly (oracle), whichever path the kernel takes.  r06: from 11 words of Q the fast
+    path holds 32 residues in registers (crt.hip crt_fast_ch): L = 16, 24, 32 in one round, L = 40 in two with the
+    check re-reading them."""
     import torch
     moduli = RNS[:L] if L == 11 else orc.gen_primes(50, 1 << 18, L)
     Q = 1
