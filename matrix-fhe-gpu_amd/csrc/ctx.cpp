@@ -292,8 +292,49 @@ static int build_wcrt(mfhe_ctx* c) {
                 num[d - 2] -= cf;
             }
         std::vector<int8_t> phi(ph.begin(), ph.end());
+        // Rader (r06): for b, j != 0 write j = g^n, b = g^-m (g = 3, a primitive root of 257); then
+        // sum_j zeta^(bj) F[j] = (a * bk)[m], the cyclic convolution of a[n] = F[g^n] and bk[k] = zeta^(g^-k), taken
+        // as IFFT_256(FFT_256(a) FFT_256(bk)): the kernel gets FFT_256(bk) / 256 (long double sums)
+        std::vector<int16_t> gp(512);
+        {
+            long x = 1;
+            for (int n = 0; n < 256; ++n) {
+                gp[n] = (int16_t)x;
+                x = x * 3 % 257;
+            }
+            long inv3 = 1;
+            for (int e = 0; e < 255; ++e) inv3 = inv3 * 3 % 257;   // 3^255 = 3^-1 mod 257
+            long y = 1;
+            for (int m = 0; m < 256; ++m) {
+                gp[256 + m] = (int16_t)y;
+                y = y * inv3 % 257;
+            }
+        }
+        std::vector<double2> rad(512);   // [0]: bk = zeta^(g^-k) (forward); [1]: its conjugate (inverse, zeta^-1)
+        {
+            const long double tp = 6.283185307179586476925286766559L;
+            std::vector<long double> br(256), bi(256), cr(256), ci(256);
+            for (int k = 0; k < 256; ++k) {
+                br[k] = cosl(tp * (long double)gp[256 + k] / 257.0L);
+                bi[k] = sinl(tp * (long double)gp[256 + k] / 257.0L);
+                cr[k] = cosl(-tp * (long double)k / 256.0L);
+                ci[k] = sinl(-tp * (long double)k / 256.0L);
+            }
+            for (int dir = 0; dir < 2; ++dir)
+                for (int k = 0; k < 256; ++k) {
+                    long double sr = 0, si = 0;
+                    for (int n = 0; n < 256; ++n) {
+                        const int e = (n * k) % 256;
+                        const long double xr = br[n], xi = dir ? -bi[n] : bi[n];
+                        sr += xr * cr[e] - xi * ci[e];
+                        si += xr * ci[e] + xi * cr[e];
+                    }
+                    rad[(size_t)dir * 256 + k] = make_double2((double)(sr / 256.0L), (double)(si / 256.0L));
+                }
+        }
         if ((rc = upload(c, &c->d_wdZ, zc)) || (rc = upload(c, &c->d_wdZi, zic)) || (rc = upload(c, &c->d_wdlam, lam)) ||
-            (rc = upload(c, &c->d_wdxp, xp)) || (rc = upload(c, &c->d_wdphi, phi)))
+            (rc = upload(c, &c->d_wdxp, xp)) || (rc = upload(c, &c->d_wdphi, phi)) || (rc = upload(c, &c->d_wdrad, rad)) ||
+            (rc = upload(c, &c->d_wdgp, gp)))
             return rc;
     }
     // i8 MFMA operand planes (gemm.hip): D balanced base-256 digits of every V / V^-1 entry, and

@@ -2084,6 +2084,250 @@ int launch_xy_fused(const double2* A, const double2* M, const double2* B, double
     return MFHE_OK;
 }
 
+// ---- the forward factored W-DFT by Rader's algorithm (r06) ----
+// cgemm_mfma_kernel<1> computes, per column p and a = a' + 1, X_a[b] = F_a[0] + sum_{j=1..256} zeta^(b j) F_a[j]
+// (b = 1..256, zeta = e^(2 pi i / 257); F_a folded from in[j] and in[j + 257] with omega = e^(2 pi i / 3)) as a
+// 256 x 256 complex GEMM.  That is a 257-point DFT: with g = 3 (a primitive root of 257), j = g^n and b = g^-m,
+// X_a[g^-m] - F_a[0] = sum_n F_a[g^n] zeta^(g^(n - m)) is the cyclic convolution of a[n] = F_a[g^n] with
+// bk[k] = zeta^(g^-k), taken as IFFT_256(FFT_256(a) . FFT_256(bk)) -- 2 x 1024 butterflies per column instead of
+// 65536 complex MACs, so the transform becomes bound by its 64 MB of HBM traffic.  Same outputs to rounding
+// (~1e-15 relative; the GEMM's are already not the reference's own rounding, HE.cu:1147-1172).
+// One workgroup: 8 columns x both a; 16 threads per column, each holding 16 points of each a's FFT: 256 = 16 x 16
+// (a 16-point radix-2 FFT in registers over s, the twiddle W256^(t k1), a transpose through LDS, the 16-point FFT
+// over t), the product with FFT(bk) / 256, and the inverse the same way.
+__device__ __forceinline__ double2 cadd(double2 x, double2 y) { return make_double2(x.x + y.x, x.y + y.y); }
+__device__ __forceinline__ double2 csub(double2 x, double2 y) { return make_double2(x.x - y.x, x.y - y.y); }
+__device__ __forceinline__ double2 cconj(double2 x) { return make_double2(x.x, -x.y); }
+// e^(SIGN 2 pi i k / 16), k = 0..7
+template <int SIGN>
+__device__ __forceinline__ double2 w16(int k) {
+    constexpr double C[8] = {1.0, 0.92387953251128675613, 0.70710678118654752440, 0.38268343236508977173,
+                             0.0, -0.38268343236508977173, -0.70710678118654752440, -0.92387953251128675613};
+    constexpr double S[8] = {0.0, 0.38268343236508977173, 0.70710678118654752440, 0.92387953251128675613,
+                             1.0, 0.92387953251128675613, 0.70710678118654752440, 0.38268343236508977173};
+    return make_double2(C[k], SIGN * S[k]);
+}
+// in-register 16-point DFT, natural order in and out: X[k] = sum_s x[s] e^(SIGN 2 pi i s k / 16)
+template <int SIGN>
+__device__ __forceinline__ void fft16(double2 (&x)[16]) {
+    auto sw = [&](int i, int j) {
+        const double2 t = x[i];
+        x[i] = x[j];
+        x[j] = t;
+    };
+    sw(1, 8); sw(2, 4); sw(3, 12); sw(5, 10); sw(7, 14); sw(11, 13);   // 4-bit reversal
+#pragma unroll
+    for (int len = 2; len <= 16; len <<= 1)
+#pragma unroll
+        for (int i = 0; i < 16; i += len)
+#pragma unroll
+            for (int j = 0; j < len / 2; ++j) {
+                const int k = j * (16 / len);
+                const double2 u = x[i + j], v = k == 0 ? x[i + j + len / 2] : cmul(x[i + j + len / 2], w16<SIGN>(k));
+                x[i + j] = cadd(u, v);
+                x[i + j + len / 2] = csub(u, v);
+            }
+}
+constexpr int RDC = 8;   // columns per workgroup
+__global__ __launch_bounds__(RDC * 16) void wdft_rader_kernel(const double2* __restrict__ in, double2* __restrict__ out,
+                                                              uint32_t Pf, const double2* __restrict__ rb,
+                                                              const int16_t* __restrict__ gp) {
+    __shared__ double2 tw[256];                  // e^(-2 pi i k / 256)
+    __shared__ double2 fb[256];                  // FFT(bk) / 256
+    __shared__ int16_t sg[512];                  // g^n, g^-m
+    __shared__ double2 xs[RDC][2][16][17];       // transposes: [column][a'][row][col], padded
+    const int t = threadIdx.x & 15, pc = threadIdx.x >> 4;
+    for (int i = threadIdx.x; i < 256; i += RDC * 16) {
+        double sn, cs;
+        sincospi(-(double)i / 128.0, &sn, &cs);
+        tw[i] = make_double2(cs, sn);
+        fb[i] = rb[i];
+        sg[i] = gp[i];
+        sg[256 + i] = gp[256 + i];
+    }
+    __syncthreads();
+    const uint32_t p = blockIdx.x * RDC + pc;
+    const bool live = p < Pf;
+    const uint32_t pr = live ? p : 0;
+    // F_a[j] for a' = 0, 1: omega^(a (j mod 3)) in[j] + omega^(a ((j + 2) mod 3)) in[j + 257] (second term if j <= 254)
+    auto fold = [&](int j, double2& f0, double2& f1) {
+        const double2 x1 = in[(uint64_t)j * Pf + pr];
+        const double2 x2 = j <= 254 ? in[(uint64_t)(j + 257) * Pf + pr] : make_double2(0.0, 0.0);
+        const int t3 = j % 3, t3b = (t3 + 2) % 3;
+        f0 = cadd(cmul(omega3(t3), x1), cmul(omega3(t3b), x2));
+        f1 = cadd(cmul(omega3((2 * t3) % 3), x1), cmul(omega3((2 * t3b) % 3), x2));
+    };
+    double2 x[2][16];
+#pragma unroll
+    for (int s = 0; s < 16; ++s) fold(sg[t + 16 * s], x[0][s], x[1][s]);
+    double2 F0[2];
+    fold(0, F0[0], F0[1]);
+    // forward FFT_256 of a[n] = F[g^n], n = t + 16 s: over s, twiddle W256^(t k1), transpose, over t
+#pragma unroll
+    for (int ap = 0; ap < 2; ++ap) {
+        fft16<-1>(x[ap]);
+#pragma unroll
+        for (int k1 = 1; k1 < 16; ++k1) x[ap][k1] = cmul(x[ap][k1], tw[(t * k1) & 255]);
+#pragma unroll
+        for (int k1 = 0; k1 < 16; ++k1) xs[pc][ap][k1][t] = x[ap][k1];
+    }
+    __syncthreads();
+#pragma unroll
+    for (int ap = 0; ap < 2; ++ap) {
+#pragma unroll
+        for (int tt = 0; tt < 16; ++tt) x[ap][tt] = xs[pc][ap][t][tt];   // this thread is now k1 = t
+        fft16<-1>(x[ap]);                                                 // A[t + 16 k2] in x[ap][k2]
+#pragma unroll
+        for (int k2 = 0; k2 < 16; ++k2) x[ap][k2] = cmul(x[ap][k2], fb[t + 16 * k2]);
+        // inverse: over k2 (this thread k1 = t) gives C[t][u]; twiddle e^(+2 pi i u t / 256); transpose; over k1
+        fft16<1>(x[ap]);
+#pragma unroll
+        for (int u = 1; u < 16; ++u) x[ap][u] = cmul(x[ap][u], cconj(tw[(u * t) & 255]));
+    }
+    __syncthreads();   // every thread has read its transposed row
+#pragma unroll
+    for (int ap = 0; ap < 2; ++ap)
+#pragma unroll
+        for (int u = 0; u < 16; ++u) xs[pc][ap][u][t] = x[ap][u];
+    __syncthreads();
+#pragma unroll
+    for (int ap = 0; ap < 2; ++ap) {
+#pragma unroll
+        for (int k1 = 0; k1 < 16; ++k1) x[ap][k1] = xs[pc][ap][t][k1];   // this thread is now u = t
+        fft16<1>(x[ap]);                                                  // y[t + 16 v] in x[ap][v]
+        if (live) {
+#pragma unroll
+            for (int v = 0; v < 16; ++v) {
+                const int b = sg[256 + t + 16 * v];   // output b = g^-m, m = t + 16 v
+                out[(uint64_t)(ap * 256 + b - 1) * Pf + p] = cadd(F0[ap], x[ap][v]);
+            }
+        }
+    }
+}
+
+// ---- the inverse factored W-DFT by Rader's algorithm (r06) ----
+// cgemm_mfma_kernel<2> + cwdft_inv_dots_kernel: E_a'[r2] = sum_{b=1..256} zeta^(-b r2) y_a'[b], y_a'[b] =
+// in[a' 256 + b - 1][p] (r2 = 0..256), then h_j = sum_a' lam1[a'][r2 mod 3] E_a'[r2] (j = r2) and
+// h_(r2+257) with lam2, c1 = h_513, c0 = h_512 - c1 phi_511, f_j = h_j - c0 phi_j - c1 phi_(j-1) (j < 512).  For
+// r2 != 0 the sum is the cyclic convolution of a[n] = y[g^n] with conj(bk) (E[g^-m] = conv[m]); E[0] = sum_b y[b]
+// is FFT(a)[0].  E at r2 = 0, 255, 256 (the c's and f_0, f_257) reach every thread of the column through LDS.
+__global__ __launch_bounds__(RDC * 16) void wdft_rader_inv_kernel(const double2* __restrict__ in, double2* __restrict__ out,
+                                                                  double* __restrict__ out_im, uint32_t Pf,
+                                                                  const double2* __restrict__ rb,
+                                                                  const int16_t* __restrict__ gp,
+                                                                  const double2* __restrict__ lam,
+                                                                  const int8_t* __restrict__ phi) {
+    __shared__ double2 tw[256];
+    __shared__ double2 fb[256];
+    __shared__ int16_t sg[512];
+    __shared__ double2 xs[RDC][2][16][17];
+    __shared__ double2 ex[RDC][2][3];            // E_a'[0], E_a'[255], E_a'[256] per column
+    const int t = threadIdx.x & 15, pc = threadIdx.x >> 4;
+    for (int i = threadIdx.x; i < 256; i += RDC * 16) {
+        double sn, cs;
+        sincospi(-(double)i / 128.0, &sn, &cs);
+        tw[i] = make_double2(cs, sn);
+        fb[i] = rb[i];
+        sg[i] = gp[i];
+        sg[256 + i] = gp[256 + i];
+    }
+    __syncthreads();
+    const uint32_t p = blockIdx.x * RDC + pc;
+    const bool live = p < Pf;
+    const uint32_t pr = live ? p : 0;
+    double2 x[2][16];
+#pragma unroll
+    for (int ap = 0; ap < 2; ++ap)
+#pragma unroll
+        for (int s = 0; s < 16; ++s) x[ap][s] = in[(uint64_t)(ap * 256 + sg[t + 16 * s] - 1) * Pf + pr];
+#pragma unroll
+    for (int ap = 0; ap < 2; ++ap) {
+        fft16<-1>(x[ap]);
+#pragma unroll
+        for (int k1 = 1; k1 < 16; ++k1) x[ap][k1] = cmul(x[ap][k1], tw[(t * k1) & 255]);
+#pragma unroll
+        for (int k1 = 0; k1 < 16; ++k1) xs[pc][ap][k1][t] = x[ap][k1];
+    }
+    __syncthreads();
+#pragma unroll
+    for (int ap = 0; ap < 2; ++ap) {
+#pragma unroll
+        for (int tt = 0; tt < 16; ++tt) x[ap][tt] = xs[pc][ap][t][tt];
+        fft16<-1>(x[ap]);
+        if (t == 0) ex[pc][ap][0] = x[ap][0];   // E[0] = sum_b y[b] = FFT(a)[0]
+#pragma unroll
+        for (int k2 = 0; k2 < 16; ++k2) x[ap][k2] = cmul(x[ap][k2], fb[t + 16 * k2]);
+        fft16<1>(x[ap]);
+#pragma unroll
+        for (int u = 1; u < 16; ++u) x[ap][u] = cmul(x[ap][u], cconj(tw[(u * t) & 255]));
+    }
+    __syncthreads();
+#pragma unroll
+    for (int ap = 0; ap < 2; ++ap)
+#pragma unroll
+        for (int u = 0; u < 16; ++u) xs[pc][ap][u][t] = x[ap][u];
+    __syncthreads();
+#pragma unroll
+    for (int ap = 0; ap < 2; ++ap) {
+#pragma unroll
+        for (int k1 = 0; k1 < 16; ++k1) x[ap][k1] = xs[pc][ap][t][k1];
+        fft16<1>(x[ap]);   // E[g^-m] for m = t + 16 v in x[ap][v]
+#pragma unroll
+        for (int v = 0; v < 16; ++v) {
+            const int r2 = sg[256 + t + 16 * v];
+            if (r2 == 255) ex[pc][ap][1] = x[ap][v];
+            if (r2 == 256) ex[pc][ap][2] = x[ap][v];
+        }
+    }
+    __syncthreads();
+    auto L = [&](int kind, int aa, int t3) { return lam[(kind * 2 + aa) * 3 + t3]; };
+    auto comb = [&](int kind, int t3, double2 e0, double2 e1) { return cadd(cmul(L(kind, 0, t3), e0), cmul(L(kind, 1, t3), e1)); };
+    const double2 E00 = ex[pc][0][0], E10 = ex[pc][1][0];
+    const double2 c1 = comb(1, 1, ex[pc][0][2], ex[pc][1][2]);                         // h_513 (r2 = 256, t = 1)
+    const double2 h512 = comb(1, 0, ex[pc][0][1], ex[pc][1][1]);                       // r2 = 255, t = 0
+    const double p511 = (double)phi[511];
+    const double2 c0 = make_double2(h512.x - c1.x * p511, h512.y - c1.y * p511);
+    if (!live) return;
+    auto put = [&](int j, double2 h) {   // f_j = h_j - c0 phi_j - c1 phi_(j-1)
+        const double f0 = (double)phi[j], f1 = j > 0 ? (double)phi[j - 1] : 0.0;
+        const double re = h.x - c0.x * f0 - c1.x * f1, im = h.y - c0.y * f0 - c1.y * f1;
+        const uint64_t idx = (uint64_t)j * Pf + p;
+        if (out_im) {
+            ((double*)out)[idx] = re;
+            out_im[idx] = im;
+        } else {
+            out[idx] = make_double2(re, im);
+        }
+    };
+#pragma unroll
+    for (int v = 0; v < 16; ++v) {
+        const int r2 = sg[256 + t + 16 * v], t3 = r2 % 3;
+        put(r2, comb(0, t3, x[0][v], x[1][v]));
+        if (r2 <= 254) put(r2 + 257, comb(1, t3, x[0][v], x[1][v]));
+    }
+    if (t == 0) {
+        put(0, comb(0, 0, E00, E10));
+        put(257, comb(1, 0, E00, E10));
+    }
+}
+
+int launch_wdft_rader_inv(const double2* in, double2* out, double* out_im, uint32_t Pf, const double2* rb,
+                          const int16_t* gp, const double2* lam, const int8_t* phi, hipStream_t s) {
+    if (!in || !out || !rb || !gp || !lam || !phi || Pf == 0 || in == out)
+        return set_error(MFHE_EINVAL, "wdft_rader_inv: bad arguments");
+    hipLaunchKernelGGL(wdft_rader_inv_kernel, dim3((Pf + RDC - 1) / RDC), dim3(RDC * 16), 0, s, in, out, out_im, Pf, rb,
+                       gp, lam, phi);
+    MFHE_CHECK_LAUNCH("wdft_rader_inv_kernel");
+    return MFHE_OK;
+}
+
+int launch_wdft_rader(const double2* in, double2* out, uint32_t Pf, const double2* rb, const int16_t* gp, hipStream_t s) {
+    if (!in || !out || !rb || !gp || Pf == 0 || in == out) return set_error(MFHE_EINVAL, "wdft_rader: bad arguments");
+    hipLaunchKernelGGL(wdft_rader_kernel, dim3((Pf + RDC - 1) / RDC), dim3(RDC * 16), 0, s, in, out, Pf, rb, gp);
+    MFHE_CHECK_LAUNCH("wdft_rader_kernel");
+    return MFHE_OK;
+}
+
 int launch_cgemm(const CGemmArgs& a, int batch, hipStream_t s) {
     dim3 grid((a.P + TP - 1) / TP, (a.M + TM - 1) / TM, batch);
     if (a.mfma) {

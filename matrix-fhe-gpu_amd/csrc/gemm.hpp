@@ -110,6 +110,13 @@ int launch_mod_gemm_smallb(const ModGemmArgs& a, const int8_t* b8, int L, hipStr
 // two independent W-CRT transforms of the same shape as one launch per step (gemm.hip; he.hip encode / decode)
 int launch_mod_gemm_pair(const ModGemmArgs& a, const ModGemmArgs& b, int L, hipStream_t s);
 int launch_cgemm(const CGemmArgs& a, int batch, hipStream_t s);
+// the forward factored W-DFT (cgemm_mfma_kernel<1>'s outputs, to rounding) by Rader's algorithm: in / out [512][Pf]
+// complex, rb = FFT_256(zeta^(g^-k)) / 256, gp = [g^n, g^-m] (mfhe_ctx d_wdrad / d_wdgp; gemm.hip)
+int launch_wdft_rader(const double2* in, double2* out, uint32_t Pf, const double2* rb, const int16_t* gp, hipStream_t s);
+// the inverse (cgemm_mfma_kernel<2> + cwdft_inv_dots_kernel, to rounding): rb = the inverse table (d_wdrad + 256),
+// lam / phi as CGemmArgs; out_im: planar output (real parts at (double*)out), else interleaved (gemm.hip)
+int launch_wdft_rader_inv(const double2* in, double2* out, double* out_im, uint32_t Pf, const double2* rb,
+                          const int16_t* gp, const double2* lam, const int8_t* phi, hipStream_t s);
 // out = A M B per lane for 64 x 64 complex blocks (A, B shared; M, out [lanes][64][64]) in one launch: the two
 // launch_cgemm products of he.hip xy3 without the intermediate's HBM round trip, the same doubles (gemm.hip)
 int launch_xy_fused(const double2* A, const double2* M, const double2* B, double2* out, int lanes, hipStream_t s);

@@ -649,10 +649,16 @@ static int wdft(mfhe_ctx* c, const double2* A, const double2* in, double2* out, 
         f.P = 2 * f.Pf;
         f.scM = g.n2;
         if (A == c->d_wdV) {
+            // mode 2: the 257-point DFTs by Rader's algorithm (gemm.hip wdft_rader_kernel, r06); 3: the GEMM
+            if (c->cgemm_mfma == 2 && c->d_wdrad && in != out)
+                return launch_wdft_rader(in, out, (uint32_t)g.n2, c->d_wdrad, c->d_wdgp, s);
             f.fac = 1;
             f.A = c->d_wdZ;
             return launch_cgemm(f, 1, s);
         }
+        if (c->cgemm_mfma == 2 && c->d_wdrad && in != out)   // Rader (gemm.hip wdft_rader_inv_kernel, r06)
+            return launch_wdft_rader_inv(in, out, planar ? (double*)out + 512ull * g.n2 : nullptr, (uint32_t)g.n2,
+                                         c->d_wdrad + 256, c->d_wdgp, c->d_wdlam, c->d_wdphi, s);
         const size_t need = (size_t)g.n2 * 2 * sizeof(double2);
         if (c->wd_ws_bytes < need) {
             if (c->wd_ws) MFHE_HIP(hipFree(c->wd_ws));

@@ -168,6 +168,9 @@ struct mfhe_ctx {
     double2* d_wdlam = nullptr;    // [2][2][3]  lam1 / lam2 [a'][t] of the inverse (771^-1 omega^-at differences)
     double2* d_wdxp = nullptr;     // [2][256]   zeta^(-255 b), zeta^(-256 b), b = 1..256
     int8_t* d_wdphi = nullptr;     // [513]      Phi_771 coefficients
+    // the forward factored W-DFT's 257-point DFTs by Rader's algorithm (gemm.hip wdft_rader_kernel, r06), g = 3:
+    double2* d_wdrad = nullptr;    // [2][256]   FFT_256(zeta^(+-g^-k mod 257)) / 256: forward, inverse
+    int16_t* d_wdgp = nullptr;     // [2][256]   g^n mod 257, g^-m mod 257
     void* wd_ws = nullptr;         // factored inverse W-DFT (c0, c1) per column, grown on demand
     size_t wd_ws_bytes = 0;
     double2 *d_encV = nullptr, *d_encVT = nullptr, *d_encVi = nullptr, *d_encViT = nullptr;  // [n][n]

@@ -159,8 +159,10 @@ def test_cgemm_mfma_matches_valu(mfhe, n):
     for i in range(2):   # XY: one launch (2) == two launches (3, 1)
         np.testing.assert_array_equal(outs[2][i], outs[3][i])
         np.testing.assert_array_equal(outs[2][i], outs[1][i])
-    for i in range(2, 4):   # the factored W-DFT of modes 2 and 3
-        np.testing.assert_array_equal(outs[2][i], outs[3][i])
+    # mode 2 takes the factored W-DFT's 257-point DFTs by Rader's algorithm (gemm.hip wdft_rader_kernel and
+    # wdft_rader_inv_kernel, r06), mode 3 by the GEMM: equal to rounding
+    for i in range(2, 4):
+        assert np.max(np.abs(outs[2][i] - outs[3][i])) <= 1e-13 * np.max(np.abs(outs[3][i])), i
     with pytest.raises(mfhe.MfheError):
         ctx.set_option(mfhe.OPT_CGEMM_MFMA, 4)
 
