@@ -120,6 +120,9 @@ int launch_wdft_rader_inv(const double2* in, double2* out, double* out_im, uint3
 // out = A M B per lane for 64 x 64 complex blocks (A, B shared; M, out [lanes][64][64]) in one launch: the two
 // launch_cgemm products of he.hip xy3 without the intermediate's HBM round trip, the same doubles (gemm.hip)
 int launch_xy_fused(const double2* A, const double2* M, const double2* B, double2* out, int lanes, hipStream_t s);
+// the same products at n = 64 by 64-point FFTs (V = ensure_xy's encoder matrix; inv: V^-1 M V^-T), equal to
+// rounding; whole lanes go through LDS, so in == out is allowed (gemm.hip xy_fft_kernel)
+int launch_xy_fft(const double2* in, double2* out, bool inv, int lanes, hipStream_t s);
 // factored inverse W-DFT, first step: per column the rows r2 = 0, 255, 256 of E_a by dot products (xpow [2][256]:
 // zeta^(-255 b), zeta^(-256 b)), then f_0, f_257 into out and (c0, c1) into a.cc (gemm.hip)
 int launch_cwdft_inv_dots(const CGemmArgs& a, const double2* in, const double2* xpow, hipStream_t s);

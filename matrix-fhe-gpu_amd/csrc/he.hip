@@ -691,9 +691,13 @@ static int wdft(mfhe_ctx* c, const double2* A, const double2* in, double2* out, 
 static int xy3(const mfhe_ctx* c, const double2* A, const double2* in, const double2* B, double2* tmp, double2* out,
                size_t lanes, hipStream_t s) {
     const Geo2 g = geo(c);
-    // n = 64 with the MFMA path: both products in one launch (gemm.hip xy_fused_kernel; MFHE_OPT_CGEMM_MFMA 3 keeps
-    // the two launches), the same doubles
-    if (c->cgemm_mfma == 2 && g.n == 64 && in != out) return launch_xy_fused(A, in, B, out, (int)lanes, s);
+    // n = 64: mode 2 by 64-point FFTs (gemm.hip xy_fft_kernel, equal to rounding); mode 3 both GEMMs in one launch
+    // (gemm.hip xy_fused_kernel), the same doubles as the two launches of mode 1
+    if (c->cgemm_mfma == 2 && g.n == 64) {
+        if (A == c->d_encV && B == c->d_encVT) return launch_xy_fft(in, out, false, (int)lanes, s);
+        if (A == c->d_encVi && B == c->d_encViT) return launch_xy_fft(in, out, true, (int)lanes, s);
+    }
+    if (c->cgemm_mfma >= 2 && g.n == 64 && in != out) return launch_xy_fused(A, in, B, out, (int)lanes, s);
     CGemmArgs a;
     a.mfma = c->cgemm_mfma != 0;
     a.M = a.K = (int)g.n;
