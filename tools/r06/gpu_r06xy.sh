@@ -2,7 +2,7 @@
 # r06xy: the tree's build against libmfhe_head.so (the previous commit's build) on tools/pipeline_bench.py,
 # alternating, then the whole final-evidence chain (gpu_r06_final.sh) on the tree's build.
 set -o pipefail
-O=gpurun_out/r06xy
+O=gpurun_out/${XYTAG:-r06xy}
 ROOT=${GRAFT_REPO_ROOT:-$(pwd)}
 mkdir -p $O
 export PYTHONUNBUFFERED=1
@@ -12,4 +12,4 @@ for r in 1 2 3; do
     python3 -c "import json,sys; d=json.loads(open('$O/pipe_${lib}_$r.json').read().strip().splitlines()[-1]); print('$lib round $r', {k: round(v, 4) for k, v in d.items() if k.endswith('_ms')})"
   done
 done
-R06TAG=${R06TAG:-r06final6} bash tools/r06/gpu_r06_final.sh
+R06TAG=${R06TAG:-r06final7} bash tools/r06/gpu_r06_final.sh
